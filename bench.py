@@ -1,0 +1,241 @@
+#!/usr/bin/env python3
+"""Headline benchmark: GiB/s CRC32C over batched 4 KiB ledger entries, device-resident.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 launched by
+torch.distributed.run, one rank per GPU. A step = one launch of the digest engine over the
+whole per-GPU batch (BASELINE.json configs[1]: 1,048,576 x 4 KiB entries, CRC32C, seed 0,
+bytes = little-endian splitmix64 stream seed 42, generated on the device). Entries shard
+across ranks with no data-path collective (weak scaling); the only collectives are the
+timing barrier and the max-over-ranks reduction.
+
+Rank 0 prints ONE JSON line with ``roofline`` (dominant kernel, HIP-event timed on its own
+stream) and, at N=1, ``cpu_baseline`` (the reference's own circe crc32c() compiled from
+/root/reference into oracle/_ref, timed on the host cores over a bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+GIB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md "Chip-level parameters"
+METRIC = "GiB/s CRC32C over batched 4 KiB ledger entries (device-resident); % HBM peak"
+
+
+def zipf_index(n: int, seed: int = 43, s: float = 1.1, kmax: int = 1024):
+    """k ~ Zipf(s) on {1..kmax} by inverse CDF over a splitmix64 stream,
+    len = max(64, 64k - (r & 63)); entries packed back to back (unaligned starts)."""
+    words = np.frombuffer(_splitmix_words(2 * n, seed), dtype=np.uint64)
+    u = (words[0::2] >> np.uint64(11)).astype(np.float64) / float(1 << 53)
+    r = words[1::2]
+    k = np.arange(1, kmax + 1, dtype=np.float64)
+    cdf = np.cumsum(k ** -s)
+    cdf /= cdf[-1]
+    kk = np.searchsorted(cdf, u, side="right") + 1
+    kk = np.minimum(kk, kmax)
+    lengths = np.maximum(64, 64 * kk - (r & np.uint64(63)).astype(np.int64)).astype(np.int64)
+    offsets = np.zeros(n, dtype=np.int64)
+    np.cumsum(lengths[:-1], out=offsets[1:])
+    return offsets, lengths
+
+
+def _splitmix_words(nwords: int, seed: int) -> bytes:
+    i = np.arange(1, nwords + 1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + i * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return z.tobytes()
+
+
+def cpu_baseline(host_sample: np.ndarray, entry_len: int, algo: int = 0, budget_s: float = 8.0):
+    """Reference circe crc32c() (oracle/_ref) over a bounded sample, all host cores we may use."""
+    import oracle
+    ref = oracle.ref()
+    n = host_sample.size // entry_len
+    out = np.zeros(n, dtype=np.uint32)
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        cores = os.cpu_count() or 1
+    cores = max(1, min(16, cores))
+    u8p = host_sample.ctypes.data_as(oracle._u8p)
+    o32 = out.ctypes.data_as(oracle._u32p)
+    if ref is not None and algo == 0:
+        kind = "reference"
+        run = lambda thr, reps: ref.ref_crc32c_uniform_timed(u8p, entry_len, entry_len, n, thr, reps, o32)
+        label = "circe crc32c() (crc32c_sse42.cpp, chunk ladder {4096,512,64}) compiled from /root/reference"
+    else:  # the C restatement (byte-table loop), single pass per rep
+        kind = "port"
+        lib = oracle.lib()
+
+        def run(thr, reps):
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                lib.oracle_uniform(algo, u8p, entry_len, entry_len, n, 0, o32)
+            return time.perf_counter() - t0
+        cores = 1
+        label = "oracle/crc_oracle.c byte-table restatement"
+    t1 = run(1, 1)  # calibrate on one core
+    one_core = host_sample.size / t1 / GIB
+    reps = max(1, int(budget_s / max(1e-6, t1 / cores)))
+    t = run(cores, reps)
+    value = host_sample.size * reps / t / GIB
+    return {"value": round(value, 3), "unit": "GiB/s", "cores": cores, "kind": kind,
+            "single_core_value": round(one_core, 3),
+            "sample": f"{n} x {entry_len} B entries of the same splitmix64 input ({host_sample.size / GIB:.3f} GiB), "
+                      f"{reps} passes over {cores} std::threads, one call per entry; {label}"}, out
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="uniform4k", choices=["uniform4k", "shard8m", "zipf"])
+    ap.add_argument("--algo", default="crc32c", choices=["crc32c", "crc32"])
+    ap.add_argument("--entries", type=int, default=0, help="entries per GPU (default by config)")
+    ap.add_argument("--lanes", type=int, default=0, help="force lanes per entry group (0 = auto)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-check", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from bookkeeper_amd import checksum as ck
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a HIP device (no CPU path exists)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    algo = ck.CRC32C if args.algo == "crc32c" else ck.CRC32
+    ck.set_group_lanes(args.lanes)
+
+    stream = torch.cuda.current_stream(dev)
+    if args.config in ("uniform4k", "shard8m"):
+        entry_len = 4096
+        n = args.entries or (1 << 20 if args.config == "uniform4k" else 8 << 20)
+        base = torch.empty(n * entry_len, dtype=torch.uint8, device=dev)
+        # the job's data is ONE global splitmix64 stream; rank r holds its slice
+        ck.fill_splitmix64(base, 42, first_word=rank * n * entry_len // 8)
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        payload_bytes = n * entry_len
+        algo_bytes = n * (entry_len + 4)  # read payload + write u32 digest
+
+        def step():
+            ck.crc_batch_uniform(algo, base, entry_len, n, out=out, stream=stream)
+        workload = {"workload": f"{n} x {entry_len} B ledger entries per GPU, device-resident, {args.algo}, seed 0",
+                    "entries_per_gpu": n, "entry_bytes": entry_len}
+    else:
+        n = args.entries or (1 << 20)
+        offs, lens = zipf_index(n)
+        total = int(offs[-1] + lens[-1])
+        base = torch.empty(total, dtype=torch.uint8, device=dev)
+        ck.fill_splitmix64(base, 42, first_word=0)
+        d_off = torch.from_numpy(offs).to(dev)
+        d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        payload_bytes = total
+        algo_bytes = total + 16 * n  # payload + 8 B offset + 4 B length + 4 B digest
+
+        def step():
+            ck.crc_batch(algo, base, d_off, d_len, out=out, stream=stream)
+        workload = {"workload": f"{n} Zipf(1.1) entries 64 B-64 KiB per GPU (mean {total / n:.0f} B), packed, "
+                                f"{args.algo}", "entries_per_gpu": n, "bytes_per_gpu": total}
+    torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        step()
+        ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = [a.elapsed_time(b) for a, b in ev]
+    avg_kernel_s = float(np.mean(kernel_ms)) / 1e3
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed_max = float(t.item())
+
+    total_payload = payload_bytes * world
+    value = total_payload / elapsed_max / GIB
+    achieved_gbs = algo_bytes / avg_kernel_s / 1e9
+    result = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed_max / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (device-generated splitmix64, seed 42)",
+        "config": dict(workload, parallelism=f"shard{world} (independent entries, no collective)",
+                       lanes=ck.lib().bkd_get_group_lanes(algo, payload_bytes // max(1, n))),
+        "hbm_peak_frac": round(value * GIB / 1e9 / (HBM_PEAK_GBS * world), 4),
+        "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic(args.config),
+                     "kernel": "crc_groups_kernel", "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
+                     "algorithmic_bytes_per_launch": algo_bytes},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config != "zipf":
+        # cpu_baseline leg: the reference timed on the host cores over a bounded sample; its
+        # digests for that sample double as a parity spot check of the GPU output.
+        m = min(n, 65536)
+        host = np.ascontiguousarray(base[: m * entry_len].cpu().numpy())
+        result["cpu_baseline"], want = cpu_baseline(host, entry_len, algo)
+        got = out[:m].cpu().numpy().view(np.uint32)
+        result["parity_check"] = {"entries": m, "match": bool((got == want).all())}
+        if not result["parity_check"]["match"]:
+            print(json.dumps(result), flush=True)
+            raise SystemExit("PARITY FAILURE: GPU digests differ from the CPU baseline's")
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _pmc_traffic(config: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), or None."""
+    path = os.path.join(HERE, "profiles", f"pmc_{config}.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        return json.load(open(path)).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,107 @@
+"""ctypes binding of libbkdigest.so (include/bkdigest.h).
+
+There is deliberately no fallback: if the HIP library is missing or no GPU is visible,
+every compute call raises. The reference's CPU providers (JNI SSE4.2 / Java9 / Java8,
+Crc32cIntChecksum.java:28-36) stay the caller's business, never a silent substitute here.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+from .build import LIB, ROOT
+
+CRC32C = 0
+CRC32 = 1
+
+BKD_OK = 0
+ERRORS = {-1: "BKD_ERR_INVALID_ARG", -2: "BKD_ERR_NO_DEVICE", -3: "BKD_ERR_HIP", -4: "BKD_ERR_BOUNDS",
+          -5: "BKD_ERR_NOMEM"}
+
+VERIFY_OK = 0
+VERIFY_TOO_SHORT = 1
+VERIFY_DIGEST_MISMATCH = 2
+VERIFY_LEDGER_MISMATCH = 3
+VERIFY_ENTRY_MISMATCH = 4
+
+HEADER_PATH = os.path.join(ROOT, "include", "bkdigest.h")
+
+
+class NativeUnavailable(RuntimeError):
+    """libbkdigest.so is missing or could not be loaded."""
+
+
+class BkdError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+_c = ctypes
+_vp = _c.c_void_p
+_u32 = _c.c_uint32
+_u64 = _c.c_uint64
+_i64 = _c.c_int64
+_int = _c.c_int
+
+# name -> (restype, argtypes); must cover every function declared in include/bkdigest.h
+PROTOTYPES = {
+    "bkd_abi_version": (_int, []),
+    "bkd_device_count": (_int, []),
+    "bkd_init": (_int, [_int]),
+    "bkd_last_error": (_c.c_char_p, []),
+    "bkd_crc_batch_uniform": (_int, [_int, _vp, _u64, _u32, _u64, _vp, _u32, _vp, _vp]),
+    "bkd_crc_batch": (_int, [_int, _vp, _u64, _vp, _vp, _u64, _vp, _u32, _vp, _vp]),
+    "bkd_stream_sync": (_int, [_vp]),
+    "bkd_crc_batch_host": (_int, [_int, _vp, _u64, _vp, _vp, _u64, _vp, _u32, _vp]),
+    "bkd_resume": (_int, [_int, _u32, _vp, _u64, _c.POINTER(_u32)]),
+    "bkd_digest_package_batch": (_int, [_int, _i64, _vp, _vp, _vp, _vp, _u64, _vp, _vp, _u64, _vp, _u64, _vp, _vp]),
+    "bkd_digest_verify_batch": (_int, [_int, _i64, _i64, _int, _vp, _u64, _vp, _vp, _u64, _vp, _vp, _vp]),
+    "bkd_fill_splitmix64": (_int, [_vp, _u64, _u64, _u64, _vp]),
+    "bkd_host_tables": (_i64, [_int, _int, _vp, _u64]),
+    "bkd_host_gf_mul": (_u32, [_int, _u32, _u32]),
+    "bkd_host_xpow8n": (_u32, [_int, _u64]),
+    "bkd_set_group_lanes": (_int, [_int]),
+    "bkd_get_group_lanes": (_int, [_int, _u64]),
+}
+
+_lib = None
+
+
+def declared_functions() -> list[str]:
+    """Function names declared in include/bkdigest.h (the ABI contract)."""
+    text = open(HEADER_PATH).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(bkd_[a-z0-9_]+)\s*\(", text)))
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            raise NativeUnavailable(f"{LIB} not built (run __graft_entry__.build() or python -m bookkeeper_amd.build)")
+        try:
+            L = ctypes.CDLL(LIB)
+        except OSError as e:  # pragma: no cover
+            raise NativeUnavailable(f"cannot load {LIB}: {e}") from e
+        for name, (res, args) in PROTOTYPES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    return (lib().bkd_last_error() or b"").decode(errors="replace")
+
+
+def check(rc: int) -> int:
+    if rc < 0:
+        raise BkdError(rc, last_error())
+    return rc
+
+
+def device_count() -> int:
+    return int(lib().bkd_device_count())

@@ -1,0 +1,48 @@
+"""Builds bookkeeper_amd/libbkdigest.so (gfx950) in-tree with hipcc.
+
+The shared library is the product: HIP kernels + the C-ABI of include/bkdigest.h.
+It is git-ignored but travels to the GPU box with the repo snapshot.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "libbkdigest.so")
+SOURCES = [os.path.join(CSRC, "bkdigest.hip")]
+DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("crc_kernels.hpp", "crc_tables.hpp")] + [
+    os.path.join(ROOT, "include", "bkdigest.h")]
+ARCH = os.environ.get("BKD_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: cannot build libbkdigest.so")
+
+
+def needs_build() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    return any(os.path.getmtime(d) > t for d in DEPS)
+
+
+def build_native(force: bool = False, extra_flags: list[str] | None = None, out: str | None = None) -> str:
+    out = out or LIB
+    if not force and out == LIB and not needs_build():
+        return out
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-I", os.path.join(ROOT, "include"), "-o", out + ".tmp"] + SOURCES + list(extra_flags or [])
+    subprocess.run(cmd, check=True)
+    os.replace(out + ".tmp", out)
+    return out
+
+
+if __name__ == "__main__":
+    print(build_native(force=True))

@@ -1,0 +1,225 @@
+"""Host-side mirror of circe-checksum's checksum facade, backed by the GPU engine.
+
+Reference surface (circe-checksum/src/main/java/com/scurrilous/circe/):
+  * ``IntHash`` (checksum/IntHash.java:23-35): calculate / resume / acceptsMemoryAddressBuffer.
+  * ``JniIntHash`` (checksum/JniIntHash.java:25-64): the provider ``Crc32cIntChecksum`` selects
+    when the native library loads; ``GpuIntHash`` below is its drop-in, reaching
+    libbkdigest.so instead of libcirce-checksum.so.
+  * ``Crc32cIntChecksum`` (checksum/Crc32cIntChecksum.java:24-100): the static facade that
+    bookkeeper-server calls (CRC32CDigestManager.java:49-56).
+  * Bounds/argument errors follow AbstractIncrementalIntHash.java:62-69
+    (negative length -> IllegalArgumentException ~ ValueError; range -> IndexOutOfBounds ~ IndexError).
+
+Values returned by the per-call API are Java ``int`` bit patterns (signed 32-bit), exactly what
+the reference returns; the batch API returns uint32 arrays.
+
+Buffers: ``bytes``/``bytearray``/``memoryview``/numpy arrays are host buffers (the reference's
+``byte[]`` / direct ``ByteBuf``); ``torch`` tensors on a HIP device are device-resident buffers
+(the new batch path). There is no CPU arithmetic in this module.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _native
+from ._native import CRC32, CRC32C, check, lib
+
+__all__ = ["CRC32C", "CRC32", "GpuIntHash", "Crc32cIntChecksum", "crc_batch", "crc_batch_uniform",
+           "crc_batch_host", "to_java_int"]
+
+
+def to_java_int(v: int) -> int:
+    v &= 0xFFFFFFFF
+    return v - (1 << 32) if v & 0x80000000 else v
+
+
+def _is_torch_tensor(x) -> bool:
+    return type(x).__module__.startswith("torch") and hasattr(x, "data_ptr")
+
+
+def _stream_ptr(stream, tensor=None):
+    if stream is not None:
+        return ctypes.c_void_p(int(getattr(stream, "cuda_stream", stream)))
+    if tensor is not None and _is_torch_tensor(tensor) and tensor.is_cuda:
+        import torch
+        return ctypes.c_void_p(int(torch.cuda.current_stream(tensor.device).cuda_stream))
+    return ctypes.c_void_p(0)
+
+
+def _host_view(buf) -> np.ndarray:
+    if isinstance(buf, np.ndarray):
+        return np.ascontiguousarray(buf).view(np.uint8).reshape(-1)
+    return np.frombuffer(memoryview(buf).cast("B"), dtype=np.uint8)
+
+
+class GpuIntHash:
+    """``IntHash`` implementation whose arithmetic runs in libbkdigest.so (JniIntHash.java:25-64)."""
+
+    def __init__(self, algo: int = CRC32C):
+        if algo not in (CRC32C, CRC32):
+            raise ValueError("unknown algorithm")
+        self.algo = algo
+        lib()  # fail loudly now if the HIP library is absent
+
+    # IntHash.calculate(ByteBuf) / calculate(ByteBuf, offset, len)  (IntHash.java:24-26)
+    def calculate(self, buffer, offset: int | None = None, length: int | None = None) -> int:
+        return self.resume(0, buffer, offset, length)
+
+    # IntHash.resume(int, ByteBuf[, offset, len]) / resume(int, byte[], offset, len)  (IntHash.java:28-32)
+    def resume(self, current: int, buffer, offset: int | None = None, length: int | None = None) -> int:
+        if offset is None:
+            offset = 0
+            length = (buffer.numel() * buffer.element_size()) if _is_torch_tensor(buffer) else len(_host_view(buffer))
+        elif length is None:
+            raise TypeError("offset given without length")
+        if length < 0:
+            raise ValueError("negative length")  # IllegalArgumentException, AbstractIncrementalIntHash.java:64-65
+        out = ctypes.c_uint32(0)
+        if _is_torch_tensor(buffer):
+            total = buffer.numel() * buffer.element_size()
+            if offset < 0 or offset + length > total:
+                raise IndexError("range outside buffer")  # AbstractIncrementalIntHash.java:66-67
+            if not buffer.is_contiguous():
+                raise ValueError("device buffer must be contiguous")
+            ptr = ctypes.c_void_p(buffer.data_ptr() + offset)
+            keep = buffer
+        else:
+            view = _host_view(buffer)
+            if offset < 0 or offset + length > view.size:
+                raise IndexError("range outside buffer")
+            keep = view
+            ptr = ctypes.c_void_p(view.ctypes.data + offset) if view.size else ctypes.c_void_p(0)
+        check(lib().bkd_resume(self.algo, current & 0xFFFFFFFF, ptr, length, ctypes.byref(out)))
+        del keep
+        return to_java_int(out.value)
+
+    # IntHash.acceptsMemoryAddressBuffer (IntHash.java:34; JniIntHash.java:60-63)
+    def acceptsMemoryAddressBuffer(self) -> bool:
+        return True
+
+    # ---- batch extension (the reference has none) ----
+    def resumeBatch(self, seeds, base, offsets, lengths, out=None, stream=None):
+        return crc_batch(self.algo, base, offsets, lengths, seeds=seeds, out=out, stream=stream)
+
+
+class Crc32cIntChecksum:
+    """Static facade (Crc32cIntChecksum.java:24-100) with the GPU provider selected."""
+
+    _hash: GpuIntHash | None = None
+
+    @classmethod
+    def _h(cls) -> GpuIntHash:
+        if cls._hash is None:
+            cls._hash = GpuIntHash(CRC32C)
+        return cls._hash
+
+    @classmethod
+    def computeChecksum(cls, payload, offset: int | None = None, length: int | None = None) -> int:
+        return cls._h().calculate(payload, offset, length)
+
+    @classmethod
+    def resumeChecksum(cls, previousChecksum: int, payload, offset: int | None = None,
+                       length: int | None = None) -> int:
+        return cls._h().resume(previousChecksum, payload, offset, length)
+
+    @classmethod
+    def acceptsMemoryAddressBuffer(cls) -> bool:
+        return cls._h().acceptsMemoryAddressBuffer()
+
+
+# ---------------------------------------------------------------------------------------------
+# Device-resident batch API (torch tensors on a HIP device)
+# ---------------------------------------------------------------------------------------------
+
+def _dev_ptr(t, name: str, dtype=None):
+    import torch
+    if t is None:
+        return ctypes.c_void_p(0)
+    if not (_is_torch_tensor(t) and t.is_cuda):
+        raise TypeError(f"{name} must be a torch tensor on a HIP device")
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError(f"{name} must have dtype {dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def crc_batch_uniform(algo: int, base, entry_len: int, n: int, stride: int | None = None, seeds=None,
+                      seed_all: int = 0, out=None, stream=None):
+    """out[i] = resume(seed_i, base[i*stride : i*stride + entry_len]) on the device."""
+    import torch
+    stride = entry_len if stride is None else stride
+    nbytes = base.numel() * base.element_size()
+    if n and (n - 1) * stride + entry_len > nbytes:
+        raise IndexError("uniform batch exceeds base buffer")
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=base.device)
+    if seeds is not None and seeds.numel() < n:
+        raise ValueError("seeds shorter than n")
+    check(lib().bkd_crc_batch_uniform(algo, _dev_ptr(base, "base"), stride, entry_len, n,
+                                      _dev_ptr(seeds, "seeds"), seed_all & 0xFFFFFFFF, _dev_ptr(out, "out"),
+                                      _stream_ptr(stream, base)))
+    return out
+
+
+def crc_batch(algo: int, base, offsets, lengths, seeds=None, seed_all: int = 0, out=None, stream=None,
+              sync_check: bool = False):
+    """out[i] = resume(seed_i, base[offsets[i] : offsets[i] + lengths[i]]) on the device.
+
+    offsets: int64 tensor, lengths: int32 tensor (values < 2^32), seeds: int32 tensor or None.
+    Out-of-range entries produce 0 and make ``bkd_stream_sync`` report BKD_ERR_BOUNDS
+    (checked here when ``sync_check``)."""
+    import torch
+    n = offsets.numel()
+    if lengths.numel() != n:
+        raise ValueError("offsets/lengths size mismatch")
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=base.device)
+    nbytes = base.numel() * base.element_size()
+    st = _stream_ptr(stream, base)
+    check(lib().bkd_crc_batch(algo, _dev_ptr(base, "base"), nbytes, _dev_ptr(offsets, "offsets", torch.int64),
+                              _dev_ptr(lengths, "lengths", torch.int32), n, _dev_ptr(seeds, "seeds"),
+                              seed_all & 0xFFFFFFFF, _dev_ptr(out, "out"), st))
+    if sync_check:
+        check(lib().bkd_stream_sync(st))
+    return out
+
+
+def crc_batch_host(algo: int, base, offsets, lengths, seeds=None, seed_all: int = 0) -> np.ndarray:
+    """Host-memory batch (H2D -> kernel -> D2H inside the library); returns uint32 CRCs."""
+    view = _host_view(base)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+    n = offsets.size
+    out = np.zeros(n, dtype=np.uint32)
+    sp = ctypes.c_void_p(0)
+    if seeds is not None:
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint32)
+        sp = ctypes.c_void_p(seeds.ctypes.data)
+    check(lib().bkd_crc_batch_host(algo, ctypes.c_void_p(view.ctypes.data if view.size else 0), view.size,
+                                   ctypes.c_void_p(offsets.ctypes.data), ctypes.c_void_p(lengths.ctypes.data), n,
+                                   sp, seed_all & 0xFFFFFFFF, ctypes.c_void_p(out.ctypes.data)))
+    return out
+
+
+def fill_splitmix64(buf, seed: int, first_word: int = 0, stream=None) -> None:
+    """Device-side synthetic input: little-endian splitmix64 words."""
+    nbytes = buf.numel() * buf.element_size()
+    check(lib().bkd_fill_splitmix64(_dev_ptr(buf, "buf"), nbytes, seed & (2**64 - 1), first_word,
+                                    _stream_ptr(stream, buf)))
+
+
+def set_group_lanes(lanes: int) -> None:
+    check(lib().bkd_set_group_lanes(lanes))
+
+
+def host_tables(algo: int, lanes: int) -> np.ndarray:
+    n = (2 + int(np.log2(lanes))) * 1024 + 256
+    out = np.zeros(n, dtype=np.uint32)
+    check(lib().bkd_host_tables(algo, lanes, ctypes.c_void_p(out.ctypes.data), n))
+    return out
+
+
+device_count = _native.device_count

@@ -1,0 +1,409 @@
+// libbkdigest.so — C-ABI over the CDNA4 CRC kernels (include/bkdigest.h).
+//
+// Runtime glue only: per-device operator-table images, launch geometry, bounds flags,
+// the host-memory staging path and the DigestManager batch framing sequence. No CPU
+// compute path exists here: without a device every entry point returns BKD_ERR_NO_DEVICE.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/bkdigest.h"
+#include "crc_kernels.hpp"
+#include "crc_tables.hpp"
+
+namespace {
+
+thread_local std::string t_err;
+
+int fail(int code, const std::string& msg) {
+    t_err = msg;
+    return code;
+}
+
+#define BKD_HIP(expr)                                                                               \
+    do {                                                                                            \
+        hipError_t e_ = (expr);                                                                     \
+        if (e_ != hipSuccess) return fail(BKD_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+constexpr int kLaneChoices[5] = {4, 8, 16, 32, 64};
+constexpr int kMaxDevices = 64;
+
+int lane_index(int lanes) {
+    for (int k = 0; k < 5; ++k)
+        if (kLaneChoices[k] == lanes) return k;
+    return -1;
+}
+
+struct DeviceState {
+    bool ready = false;
+    int cus = 0;
+    uint32_t* tables[2][5] = {};  // [algo][lane choice] compact operator images
+    uint32_t* err = nullptr;      // sticky bounds-violation flag for indexed batches
+};
+
+std::mutex g_mu;
+DeviceState g_dev[kMaxDevices];
+std::atomic<int> g_forced_lanes{0};
+
+int current_device(int* dev) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return fail(BKD_ERR_NO_DEVICE, "no HIP device");
+    BKD_HIP(hipGetDevice(dev));
+    if (*dev < 0 || *dev >= kMaxDevices) return fail(BKD_ERR_NO_DEVICE, "device index out of range");
+    return BKD_OK;
+}
+
+int init_device_locked(int dev) {
+    DeviceState& ds = g_dev[dev];
+    if (ds.ready) return BKD_OK;
+    int prev = 0;
+    BKD_HIP(hipGetDevice(&prev));
+    BKD_HIP(hipSetDevice(dev));
+    hipDeviceProp_t prop;
+    BKD_HIP(hipGetDeviceProperties(&prop, dev));
+    ds.cus = prop.multiProcessorCount;
+    std::vector<uint32_t> img;
+    for (int algo = 0; algo < 2; ++algo) {
+        for (int k = 0; k < 5; ++k) {
+            const int lanes = kLaneChoices[k];
+            img.assign((size_t)bkd::gf2::compact_words(lanes), 0u);
+            bkd::gf2::build_compact(algo, lanes, img.data());
+            BKD_HIP(hipMalloc(&ds.tables[algo][k], img.size() * sizeof(uint32_t)));
+            BKD_HIP(hipMemcpy(ds.tables[algo][k], img.data(), img.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        }
+    }
+    BKD_HIP(hipMalloc(&ds.err, sizeof(uint32_t)));
+    BKD_HIP(hipMemset(ds.err, 0, sizeof(uint32_t)));
+    BKD_HIP(hipSetDevice(prev));
+    ds.ready = true;
+    return BKD_OK;
+}
+
+int ensure_current(DeviceState** out) {
+    int dev = 0;
+    int rc = current_device(&dev);
+    if (rc) return rc;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        rc = init_device_locked(dev);
+    }
+    if (rc) return rc;
+    *out = &g_dev[dev];
+    return BKD_OK;
+}
+
+int auto_lanes(uint64_t mean_len) {
+    const int forced = g_forced_lanes.load();
+    if (forced) return forced;
+    if (mean_len < 1024) return 4;
+    if (mean_len < 16384) return 8;
+    if (mean_len < 65536) return 16;
+    return 32;
+}
+
+constexpr int kPF = 4;
+constexpr bool kNT = false;
+
+template <int G, class Src>
+int launch_groups(DeviceState& ds, int algo, const uint8_t* base, const Src& src, uint64_t n, uint32_t* out,
+                  hipStream_t stream) {
+    if (n == 0) return BKD_OK;
+    const uint64_t groups_per_block = bkd::kBlock / G;
+    uint64_t blocks = (n + groups_per_block - 1) / groups_per_block;
+    blocks = std::min<uint64_t>(blocks, (uint64_t)ds.cus);
+    const uint32_t* tab = ds.tables[algo][lane_index(G)];
+    hipLaunchKernelGGL((bkd::crc_groups_kernel<G, kPF, kNT, Src>), dim3((unsigned)blocks), dim3(bkd::kBlock), 0,
+                       stream, base, src, n, tab, out, ds.err);
+    BKD_HIP(hipGetLastError());
+    return BKD_OK;
+}
+
+template <class Src>
+int dispatch_lanes(DeviceState& ds, int lanes, int algo, const uint8_t* base, const Src& src, uint64_t n,
+                   uint32_t* out, hipStream_t stream) {
+    switch (lanes) {
+        case 4: return launch_groups<4>(ds, algo, base, src, n, out, stream);
+        case 8: return launch_groups<8>(ds, algo, base, src, n, out, stream);
+        case 16: return launch_groups<16>(ds, algo, base, src, n, out, stream);
+        case 32: return launch_groups<32>(ds, algo, base, src, n, out, stream);
+        case 64: return launch_groups<64>(ds, algo, base, src, n, out, stream);
+        default: return fail(BKD_ERR_INVALID_ARG, "lanes must be 4, 8, 16, 32 or 64");
+    }
+}
+
+bool valid_algo(int algo) { return algo == BKD_CRC32C || algo == BKD_CRC32; }
+
+bool is_device_pointer(const void* p) {
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bkd_abi_version(void) { return BKD_ABI_VERSION; }
+
+int bkd_device_count(void) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return count;
+}
+
+int bkd_init(int device) {
+    int count = bkd_device_count();
+    if (count <= 0) return fail(BKD_ERR_NO_DEVICE, "no HIP device");
+    if (device < 0 || device >= count || device >= kMaxDevices) return fail(BKD_ERR_INVALID_ARG, "bad device");
+    std::lock_guard<std::mutex> lk(g_mu);
+    return init_device_locked(device);
+}
+
+const char* bkd_last_error(void) { return t_err.c_str(); }
+
+int bkd_set_group_lanes(int lanes) {
+    if (lanes != 0 && lane_index(lanes) < 0) return fail(BKD_ERR_INVALID_ARG, "lanes must be 0, 4, 8, 16, 32 or 64");
+    g_forced_lanes.store(lanes);
+    return BKD_OK;
+}
+
+int bkd_get_group_lanes(int algo, uint64_t mean_len) {
+    (void)algo;
+    return auto_lanes(mean_len);
+}
+
+int bkd_crc_batch_uniform(int algo, const void* d_base, uint64_t stride, uint32_t entry_len, uint64_t n,
+                          const uint32_t* d_seeds, uint32_t seed_all, uint32_t* d_out, void* stream) {
+    if (!valid_algo(algo)) return fail(BKD_ERR_INVALID_ARG, "unknown algorithm");
+    if (n && (!d_base || !d_out)) return fail(BKD_ERR_INVALID_ARG, "null buffer");
+    if (n > 1 && stride < entry_len) return fail(BKD_ERR_INVALID_ARG, "stride < entry_len");
+    DeviceState* ds = nullptr;
+    int rc = ensure_current(&ds);
+    if (rc) return rc;
+    bkd::UniformSrc src{stride, entry_len, d_seeds, seed_all};
+    return dispatch_lanes(*ds, auto_lanes(entry_len), algo, (const uint8_t*)d_base, src, n, d_out,
+                          (hipStream_t)stream);
+}
+
+int bkd_crc_batch(int algo, const void* d_base, uint64_t base_size, const uint64_t* d_offsets,
+                  const uint32_t* d_lengths, uint64_t n, const uint32_t* d_seeds, uint32_t seed_all,
+                  uint32_t* d_out, void* stream) {
+    if (!valid_algo(algo)) return fail(BKD_ERR_INVALID_ARG, "unknown algorithm");
+    if (n && (!d_offsets || !d_lengths || !d_out)) return fail(BKD_ERR_INVALID_ARG, "null index/out");
+    if (n && !d_base && base_size) return fail(BKD_ERR_INVALID_ARG, "null base");
+    DeviceState* ds = nullptr;
+    int rc = ensure_current(&ds);
+    if (rc) return rc;
+    const uint64_t mean = n ? base_size / n : 0;
+    bkd::IndexedSrc src{d_offsets, d_lengths, d_seeds, seed_all, base_size};
+    return dispatch_lanes(*ds, auto_lanes(mean), algo, (const uint8_t*)d_base, src, n, d_out, (hipStream_t)stream);
+}
+
+int bkd_stream_sync(void* stream) {
+    DeviceState* ds = nullptr;
+    int rc = ensure_current(&ds);
+    if (rc) return rc;
+    BKD_HIP(hipStreamSynchronize((hipStream_t)stream));
+    uint32_t flag = 0;
+    BKD_HIP(hipMemcpy(&flag, ds->err, sizeof(flag), hipMemcpyDeviceToHost));
+    if (flag) {
+        BKD_HIP(hipMemset(ds->err, 0, sizeof(uint32_t)));
+        return fail(BKD_ERR_BOUNDS, "an indexed entry exceeded its base buffer (entries skipped, out = 0)");
+    }
+    return BKD_OK;
+}
+
+int bkd_crc_batch_host(int algo, const void* h_base, uint64_t base_size, const uint64_t* h_offsets,
+                       const uint32_t* h_lengths, uint64_t n, const uint32_t* h_seeds, uint32_t seed_all,
+                       uint32_t* h_out) {
+    if (!valid_algo(algo)) return fail(BKD_ERR_INVALID_ARG, "unknown algorithm");
+    if (n == 0) return BKD_OK;
+    if (!h_offsets || !h_lengths || !h_out || (!h_base && base_size)) return fail(BKD_ERR_INVALID_ARG, "null buffer");
+    for (uint64_t i = 0; i < n; ++i)
+        if (h_offsets[i] > base_size || (uint64_t)h_lengths[i] > base_size - h_offsets[i])
+            return fail(BKD_ERR_BOUNDS, "entry " + std::to_string(i) + " exceeds base buffer");
+    DeviceState* ds = nullptr;
+    int rc = ensure_current(&ds);
+    if (rc) return rc;
+    hipStream_t st;
+    BKD_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    uint8_t* d_base = nullptr;
+    uint64_t* d_off = nullptr;
+    uint32_t *d_len = nullptr, *d_seeds = nullptr, *d_out = nullptr;
+    auto cleanup = [&]() {
+        (void)hipStreamSynchronize(st);
+        if (d_base) (void)hipFree(d_base);
+        if (d_off) (void)hipFree(d_off);
+        if (d_len) (void)hipFree(d_len);
+        if (d_seeds) (void)hipFree(d_seeds);
+        if (d_out) (void)hipFree(d_out);
+        (void)hipStreamDestroy(st);
+    };
+    hipError_t e = hipSuccess;
+    if (base_size) e = hipMalloc(&d_base, base_size);
+    if (e == hipSuccess) e = hipMalloc(&d_off, n * 8);
+    if (e == hipSuccess) e = hipMalloc(&d_len, n * 4);
+    if (e == hipSuccess) e = hipMalloc(&d_out, n * 4);
+    if (e == hipSuccess && h_seeds) e = hipMalloc(&d_seeds, n * 4);
+    if (e == hipSuccess && base_size) e = hipMemcpyAsync(d_base, h_base, base_size, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_off, h_offsets, n * 8, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_len, h_lengths, n * 4, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess && h_seeds) e = hipMemcpyAsync(d_seeds, h_seeds, n * 4, hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) {
+        cleanup();
+        return fail(BKD_ERR_HIP, std::string("host batch staging: ") + hipGetErrorString(e));
+    }
+    const uint64_t mean = base_size / n;
+    bkd::IndexedSrc src{d_off, d_len, d_seeds, seed_all, base_size};
+    rc = dispatch_lanes(*ds, auto_lanes(mean), algo, d_base, src, n, d_out, st);
+    if (rc == BKD_OK) {
+        e = hipMemcpyAsync(h_out, d_out, n * 4, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) rc = fail(BKD_ERR_HIP, std::string("host batch: ") + hipGetErrorString(e));
+    }
+    cleanup();
+    return rc;
+}
+
+int bkd_resume(int algo, uint32_t current, const void* ptr, uint64_t len, uint32_t* out) {
+    if (!valid_algo(algo)) return fail(BKD_ERR_INVALID_ARG, "unknown algorithm");
+    if (!out) return fail(BKD_ERR_INVALID_ARG, "null out");
+    if (len > 0xFFFFFFFFull) return fail(BKD_ERR_INVALID_ARG, "len > 4 GiB - 1");
+    if (len == 0) {  // crc32c_sse42.cpp:211-213: resume of nothing returns the seed
+        DeviceState* ds = nullptr;
+        int rc = ensure_current(&ds);
+        if (rc) return rc;
+        *out = current;
+        return BKD_OK;
+    }
+    if (!ptr) return fail(BKD_ERR_INVALID_ARG, "null buffer");
+    const uint64_t off = 0;
+    const uint32_t l32 = (uint32_t)len;
+    if (is_device_pointer(ptr)) {
+        DeviceState* ds = nullptr;
+        int rc = ensure_current(&ds);
+        if (rc) return rc;
+        uint64_t* d_off = nullptr;
+        uint32_t *d_len = nullptr, *d_out = nullptr;
+        BKD_HIP(hipMalloc(&d_off, 8));
+        BKD_HIP(hipMalloc(&d_len, 4));
+        BKD_HIP(hipMalloc(&d_out, 4));
+        BKD_HIP(hipMemcpy(d_off, &off, 8, hipMemcpyHostToDevice));
+        BKD_HIP(hipMemcpy(d_len, &l32, 4, hipMemcpyHostToDevice));
+        bkd::IndexedSrc src{d_off, d_len, nullptr, current, len};
+        rc = dispatch_lanes(*ds, auto_lanes(len), algo, (const uint8_t*)ptr, src, 1, d_out, nullptr);
+        if (rc == BKD_OK) {
+            hipError_t e = hipMemcpy(out, d_out, 4, hipMemcpyDeviceToHost);
+            if (e != hipSuccess) rc = fail(BKD_ERR_HIP, hipGetErrorString(e));
+        }
+        (void)hipFree(d_off);
+        (void)hipFree(d_len);
+        (void)hipFree(d_out);
+        return rc;
+    }
+    return bkd_crc_batch_host(algo, ptr, len, &off, &l32, 1, nullptr, current, out);
+}
+
+int bkd_digest_package_batch(int algo, int64_t ledger_id, const int64_t* d_entry_ids, const int64_t* d_lacs,
+                             const int64_t* d_length_fields, const void* d_payload, uint64_t payload_size,
+                             const uint64_t* d_offsets, const uint32_t* d_lengths, uint64_t n, void* d_frames,
+                             uint64_t frame_stride, uint32_t* d_digests, void* stream) {
+    if (!valid_algo(algo)) return fail(BKD_ERR_INVALID_ARG, "unknown algorithm");
+    const uint32_t mac = algo == BKD_CRC32C ? 4u : 8u;
+    if (n == 0) return BKD_OK;
+    if (!d_entry_ids || !d_lacs || !d_length_fields || !d_offsets || !d_lengths || !d_frames || !d_digests)
+        return fail(BKD_ERR_INVALID_ARG, "null buffer");
+    if (frame_stride < 32u + mac) return fail(BKD_ERR_INVALID_ARG, "frame_stride < 32 + digest length");
+    DeviceState* ds = nullptr;
+    int rc = ensure_current(&ds);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    const int lanes = auto_lanes(payload_size / n);
+    const uint32_t* tab = ds->tables[algo][lane_index(lanes)];
+    const uint32_t* btab = tab + (bkd::gf2::compact_words(lanes) - 256);
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(bkd::package_header_kernel, dim3(blocks), dim3(256), 0, st, btab, ledger_id, d_entry_ids,
+                       d_lacs, d_length_fields, n, (uint8_t*)d_frames, frame_stride, d_digests);
+    BKD_HIP(hipGetLastError());
+    bkd::IndexedSrc src{d_offsets, d_lengths, d_digests, 0u, payload_size};
+    rc = dispatch_lanes(*ds, lanes, algo, (const uint8_t*)d_payload, src, n, d_digests, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(bkd::package_digest_kernel, dim3(blocks), dim3(256), 0, st, d_digests, n,
+                       (uint8_t*)d_frames, frame_stride, mac);
+    BKD_HIP(hipGetLastError());
+    return BKD_OK;
+}
+
+int bkd_digest_verify_batch(int algo, int64_t ledger_id, int64_t first_entry_id, int skip_entry_check,
+                            const void* d_framed, uint64_t framed_size, const uint64_t* d_offsets,
+                            const uint32_t* d_lengths, uint64_t n, int32_t* d_status, uint64_t* d_first_bad,
+                            void* stream) {
+    if (!valid_algo(algo)) return fail(BKD_ERR_INVALID_ARG, "unknown algorithm");
+    const uint32_t mac = algo == BKD_CRC32C ? 4u : 8u;
+    if (!d_first_bad) return fail(BKD_ERR_INVALID_ARG, "null first_bad");
+    if (n && (!d_offsets || !d_lengths || !d_status)) return fail(BKD_ERR_INVALID_ARG, "null buffer");
+    DeviceState* ds = nullptr;
+    int rc = ensure_current(&ds);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    if (n == 0) {
+        BKD_HIP(hipMemsetAsync(d_first_bad, 0, sizeof(uint64_t), st));
+        return BKD_OK;
+    }
+    const int lanes = auto_lanes(framed_size / n);
+    const uint32_t* tab = ds->tables[algo][lane_index(lanes)];
+    const uint32_t* btab = tab + (bkd::gf2::compact_words(lanes) - 256);
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    uint32_t* scratch = reinterpret_cast<uint32_t*>(d_status);
+    hipLaunchKernelGGL(bkd::verify_header_kernel, dim3(blocks), dim3(256), 0, st, btab, (const uint8_t*)d_framed,
+                       framed_size, d_offsets, d_lengths, n, mac, scratch, d_first_bad);
+    BKD_HIP(hipGetLastError());
+    bkd::FramedPayloadSrc src{d_offsets, d_lengths, scratch, framed_size, mac};
+    rc = dispatch_lanes(*ds, lanes, algo, (const uint8_t*)d_framed, src, n, scratch, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(bkd::verify_finish_kernel, dim3(blocks), dim3(256), 0, st, (const uint8_t*)d_framed,
+                       framed_size, d_offsets, d_lengths, n, mac, ledger_id, first_entry_id, skip_entry_check,
+                       d_status, (unsigned long long*)d_first_bad);
+    BKD_HIP(hipGetLastError());
+    return BKD_OK;
+}
+
+int bkd_fill_splitmix64(void* d_dst, uint64_t nbytes, uint64_t seed, uint64_t first_word, void* stream) {
+    if (nbytes == 0) return BKD_OK;
+    if (!d_dst) return fail(BKD_ERR_INVALID_ARG, "null buffer");
+    DeviceState* ds = nullptr;
+    int rc = ensure_current(&ds);
+    if (rc) return rc;
+    const uint64_t nw = std::max<uint64_t>(1, nbytes / 8);
+    const unsigned blocks = (unsigned)std::min<uint64_t>((nw + 255) / 256, (uint64_t)ds->cus * 16);
+    hipLaunchKernelGGL(bkd::fill_splitmix64_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                       (uint8_t*)d_dst, nbytes, seed, first_word);
+    BKD_HIP(hipGetLastError());
+    return BKD_OK;
+}
+
+int64_t bkd_host_tables(int algo, int lanes, uint32_t* out, uint64_t out_words) {
+    if (!valid_algo(algo) || lane_index(lanes) < 0) return fail(BKD_ERR_INVALID_ARG, "bad algo/lanes");
+    const int64_t need = bkd::gf2::compact_words(lanes);
+    if (!out || out_words < (uint64_t)need) return fail(BKD_ERR_INVALID_ARG, "output too small");
+    return bkd::gf2::build_compact(algo, lanes, out);
+}
+
+uint32_t bkd_host_gf_mul(int algo, uint32_t a, uint32_t b) { return bkd::gf2::mul(algo, a, b); }
+
+uint32_t bkd_host_xpow8n(int algo, uint64_t nbytes) { return bkd::gf2::xpow(algo, nbytes * 8); }
+
+}  // extern "C"

@@ -1,0 +1,423 @@
+// CDNA4 (gfx950) CRC32C / CRC32 batch kernels — one CRC per ledger entry.
+//
+// Replaces the per-entry host scan of circe-checksum (crc32c(), circe-checksum/src/main/
+// circe/cpp/crc32c_sse42.cpp:184-217, hot loop :100-104) with a batched byte scan over
+// HBM-resident entries. Design:
+//
+//  * A GROUP of G lanes (G | 64) owns one entry at a time. Its window is END-aligned:
+//    J = ceil(len / 16G) steps; at step j lane g loads the 16 bytes at
+//    end - 16G*(J-j) + 16g with one global_load_dwordx4. Bytes in front of the entry
+//    (head of step 0) are zero, which leaves a zero-initialised CRC register unchanged,
+//    so no length-dependent shift is ever needed.
+//  * Each lane keeps 4 independent dword streams; every stream advances by the same
+//    operator C = x^(128G) ("skip 16G bytes"), so ONE operator table set serves all
+//    streams: acc = acc*C ^ dword. The 4 byte tables of C are replicated 32x in LDS with
+//    entry b of table t for bank k at byte (t>>1)*64Ki + b*256 + (t&1)*128 + 4k; lane k of
+//    each 32-lane half reads only bank k, so the random-index lookups are bank-conflict free.
+//    One v_perm_b32 builds each lookup address (byte index -> bits 8..15, lane bank -> bits 2..6).
+//  * The seed is folded into the data: XOR ~seed into the entry's first 4 bytes
+//    (reg(r, D) = reg(0, D ^ r||0...)), valid for len >= 4; entries < 16 B take a serial path.
+//  * Finish: in-lane Horner over the 4 streams with x^32, a log2(G) shuffle tree with
+//    x^(128*2^s), a final x^32, complement. Those operator tables are compact (unreplicated).
+//
+// The reference merges streams the same way with its shift tables (crc32c_sse42.cpp:107-126,
+// make_shift_table :82-90); here the merge operators are per lane tree level.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bkd {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBlock = 1024;          // 16 waves per CU, one workgroup per CU (LDS-limited)
+constexpr uint32_t kMainBytes = 131072u;  // 4 tables x 256 entries x 32 banks x 4 B
+
+template <int G>
+struct Geo {
+    static_assert(G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "group width");
+    static constexpr int kLevels = G == 4 ? 2 : G == 8 ? 3 : G == 16 ? 4 : G == 32 ? 5 : 6;
+    static constexpr int kCompactWords = (2 + kLevels) * 1024 + 256;
+    static constexpr int kAuxWords = kCompactWords - 1024;  // everything but the main operator
+    static constexpr uint32_t kX32Off = kMainBytes;         // LDS byte offset of the x^32 set
+    static constexpr uint32_t kByteTabOff = kMainBytes + (1 + kLevels) * 4096u;
+    static constexpr int kLdsWords = (int)(kMainBytes / 4) + kAuxWords;
+    static constexpr int64_t kStep = 16 * G;
+};
+
+__device__ __forceinline__ uint32_t lds_word(const uint32_t* lds, uint32_t byte_addr) {
+    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + byte_addr);
+}
+
+// v * C_main via the replicated tables. lanereg = 4*(lane&31) | 1<<16.
+// v_perm_b32 result bytes (b3..b0) = (0, hi, v.byte_t, 4*(lane&31)); hi = 1 selects the
+// upper 64 KiB half (tables 2, 3); the +128 immediate selects the odd table of a pair.
+__device__ __forceinline__ uint32_t mul_main(const uint32_t* lds, uint32_t v, uint32_t lanereg) {
+    const uint32_t a0 = __builtin_amdgcn_perm(v, lanereg, 0x0C0C0400u);
+    const uint32_t a1 = __builtin_amdgcn_perm(v, lanereg, 0x0C0C0500u);
+    const uint32_t a2 = __builtin_amdgcn_perm(v, lanereg, 0x0C020600u);
+    const uint32_t a3 = __builtin_amdgcn_perm(v, lanereg, 0x0C020700u);
+    return lds_word(lds, a0) ^ lds_word(lds, a1 + 128u) ^ lds_word(lds, a2) ^ lds_word(lds, a3 + 128u);
+}
+
+// v * C via a compact 4x256 operator set at LDS byte offset `off`.
+__device__ __forceinline__ uint32_t mul_aux(const uint32_t* lds, uint32_t off, uint32_t v) {
+    return lds_word(lds, off + ((v & 0xffu) << 2)) ^ lds_word(lds, off + 1024u + (((v >> 8) & 0xffu) << 2)) ^
+           lds_word(lds, off + 2048u + (((v >> 16) & 0xffu) << 2)) ^
+           lds_word(lds, off + 3072u + ((v >> 24) << 2));
+}
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(const uint8_t* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    else return *reinterpret_cast<const u32x4*>(p);
+}
+
+// 128-bit left shift by d bytes (1..15): out byte k = in byte k-d, zeros below.
+__device__ __forceinline__ u32x4 shl_bytes(u32x4 v, uint32_t d) {
+    uint64_t lo = (uint64_t)v.x | ((uint64_t)v.y << 32);
+    uint64_t hi = (uint64_t)v.z | ((uint64_t)v.w << 32);
+    const uint32_t sh = d * 8u;
+    if (sh >= 64u) {
+        hi = lo << (sh - 64u);
+        lo = 0;
+    } else {
+        hi = (hi << sh) | (lo >> (64u - sh));
+        lo <<= sh;
+    }
+    u32x4 r;
+    r.x = (uint32_t)lo; r.y = (uint32_t)(lo >> 32); r.z = (uint32_t)hi; r.w = (uint32_t)(hi >> 32);
+    return r;
+}
+
+// The part of the 4-byte register image r that lands in the dword starting d bytes
+// before it (d in [-3, 3], little-endian), else 0.
+__device__ __forceinline__ uint32_t place_seed(uint32_t r, int64_t d) {
+    if (d >= 0 && d <= 3) return r << (8 * (uint32_t)d);
+    if (d < 0 && d >= -3) return r >> (8 * (uint32_t)(-d));
+    return 0u;
+}
+
+// ---- entry sources: where entry i lives, how long it is, what it resumes from ----
+// get() returns 0 = compute, 1 = skip (out = 0), 2 = out of bounds (out = 0, flag).
+
+struct UniformSrc {
+    uint64_t stride;
+    uint32_t len;
+    const uint32_t* seeds;
+    uint32_t seed_all;
+    __device__ __forceinline__ int get(uint64_t i, int64_t& off, uint32_t& n, uint32_t& seed) const {
+        off = (int64_t)(i * stride);
+        n = len;
+        seed = seeds ? seeds[i] : seed_all;
+        return 0;
+    }
+};
+
+struct IndexedSrc {
+    const uint64_t* offsets;
+    const uint32_t* lengths;
+    const uint32_t* seeds;
+    uint32_t seed_all;
+    uint64_t size;
+    __device__ __forceinline__ int get(uint64_t i, int64_t& off, uint32_t& n, uint32_t& seed) const {
+        const uint64_t o = offsets[i];
+        const uint32_t l = lengths[i];
+        if (o > size || (uint64_t)l > size - o) return 2;
+        off = (int64_t)o;
+        n = l;
+        seed = seeds ? seeds[i] : seed_all;
+        return 0;
+    }
+};
+
+// Framed entry [32 B header][mac][payload]: CRC the payload resuming from the header CRC
+// already stored in seeds[i] (DigestManager.java:236-239).
+struct FramedPayloadSrc {
+    const uint64_t* offsets;
+    const uint32_t* lengths;
+    const uint32_t* seeds;
+    uint64_t size;
+    uint32_t mac;
+    __device__ __forceinline__ int get(uint64_t i, int64_t& off, uint32_t& n, uint32_t& seed) const {
+        const uint64_t o = offsets[i];
+        const uint32_t l = lengths[i];
+        if (o > size || (uint64_t)l > size - o) return 2;
+        if (l < 32u + mac) return 1;
+        off = (int64_t)(o + 32u + mac);
+        n = l - 32u - mac;
+        seed = seeds[i];
+        return 0;
+    }
+};
+
+template <int G, int PF, bool NT, class Src>
+__global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __restrict__ base, Src src, uint64_t n,
+                                                            const uint32_t* __restrict__ tables,
+                                                            uint32_t* __restrict__ out, uint32_t* __restrict__ err) {
+    using Gm = Geo<G>;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[Gm::kLdsWords];
+
+    // Stage the operator tables: main operator replicated per bank, the rest compact.
+    for (int idx = threadIdx.x; idx < 4 * 256 * 8; idx += kBlock) {
+        const int q = idx & 7, b = (idx >> 3) & 255, t = idx >> 11;
+        const uint32_t v = tables[t * 256 + b];
+        const uint32_t addr = (uint32_t)(t >> 1) * 65536u + (uint32_t)b * 256u + (uint32_t)(t & 1) * 128u +
+                              (uint32_t)q * 16u;
+        *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(lds) + addr) = u32x4{v, v, v, v};
+    }
+    for (int idx = threadIdx.x; idx < Gm::kAuxWords; idx += kBlock) lds[kMainBytes / 4 + idx] = tables[1024 + idx];
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const int g = lane & (G - 1);
+    const uint32_t lanereg = ((uint32_t)(lane & 31) << 2) | (1u << 16);
+    const uint64_t ngroups = (uint64_t)gridDim.x * (kBlock / G);
+    const uint64_t gid = (uint64_t)blockIdx.x * (kBlock / G) + (uint64_t)(threadIdx.x / G);
+
+    for (uint64_t i = gid; i < n; i += ngroups) {
+        int64_t s;
+        uint32_t len, seed;
+        const int st = src.get(i, s, len, seed);
+        if (st != 0) {
+            if (g == 0) {
+                out[i] = 0u;
+                if (st == 2 && err) atomicOr(err, 1u);
+            }
+            continue;
+        }
+        if (len < 16u) {  // tiny entry: serial byte loop (ReflectedIntCrc.java:44-48 form)
+            if (g == 0) {
+                uint32_t r = ~seed;
+                const uint8_t* q = base + s;
+                for (uint32_t k = 0; k < len; ++k)
+                    r = lds_word(lds, Gm::kByteTabOff + (((r ^ q[k]) & 0xffu) << 2)) ^ (r >> 8);
+                out[i] = ~r;
+            }
+            continue;
+        }
+
+        const uint32_t J = (uint32_t)((len + Gm::kStep - 1) / Gm::kStep);
+        const int64_t e = s + (int64_t)len;
+        const int64_t a = e - (int64_t)J * Gm::kStep + 16 * g;
+
+        // Step 0: masked head + seed fold.
+        u32x4 w;
+        if (a >= s) {
+            w = ld16<NT>(base + a);
+        } else if (a + 16 > s) {
+            w = shl_bytes(ld16<NT>(base + s), (uint32_t)(s - a));
+        } else {
+            w = u32x4{0u, 0u, 0u, 0u};
+        }
+        if (a < s + 4 && a + 16 > s) {
+            const uint32_t r0 = ~seed;
+            const int64_t d = s - a;
+            w.x ^= place_seed(r0, d);
+            w.y ^= place_seed(r0, d - 4);
+            w.z ^= place_seed(r0, d - 8);
+            w.w ^= place_seed(r0, d - 12);
+        }
+        uint32_t c0 = w.x, c1 = w.y, c2 = w.z, c3 = w.w;
+
+        // Steps 1..J-1 with PF loads in flight per lane. The steady-state loop issues its
+        // loads unconditionally (a conditional load would merge registers and force an
+        // early vmcnt(0)); only the < PF-step tail is handled with guarded code.
+        const uint8_t* p = base + a + Gm::kStep;
+        const uint32_t rem = J - 1u;
+#define BKD_FOLD(d)                                  \
+    do {                                             \
+        c0 = mul_main(lds, c0, lanereg) ^ (d).x;     \
+        c1 = mul_main(lds, c1, lanereg) ^ (d).y;     \
+        c2 = mul_main(lds, c2, lanereg) ^ (d).z;     \
+        c3 = mul_main(lds, c3, lanereg) ^ (d).w;     \
+    } while (0)
+        if (rem >= (uint32_t)PF) {
+            // A/B register double buffer: fold one block while the other block's loads fly.
+            u32x4 A[PF], B[PF];
+#pragma unroll
+            for (int k = 0; k < PF; ++k) A[k] = ld16<NT>(p + (int64_t)k * Gm::kStep);
+            p += (int64_t)PF * Gm::kStep;  // p = first step not yet loaded
+            uint32_t left = rem - (uint32_t)PF;
+            while (left >= 2u * PF) {
+#pragma unroll
+                for (int k = 0; k < PF; ++k) B[k] = ld16<NT>(p + (int64_t)k * Gm::kStep);
+#pragma unroll
+                for (int k = 0; k < PF; ++k) BKD_FOLD(A[k]);
+#pragma unroll
+                for (int k = 0; k < PF; ++k) A[k] = ld16<NT>(p + (int64_t)(PF + k) * Gm::kStep);
+#pragma unroll
+                for (int k = 0; k < PF; ++k) BKD_FOLD(B[k]);
+                p += (int64_t)(2 * PF) * Gm::kStep;
+                left -= 2u * PF;
+            }
+            // Tail: A holds PF loaded steps; `left` (< 2PF) steps remain unloaded.
+#pragma unroll
+            for (int k = 0; k < PF; ++k)
+                if ((uint32_t)k < left) B[k] = ld16<NT>(p + (int64_t)k * Gm::kStep);
+#pragma unroll
+            for (int k = 0; k < PF; ++k) BKD_FOLD(A[k]);
+#pragma unroll
+            for (int k = 0; k < PF; ++k)
+                if ((uint32_t)(PF + k) < left) A[k] = ld16<NT>(p + (int64_t)(PF + k) * Gm::kStep);
+#pragma unroll
+            for (int k = 0; k < PF; ++k)
+                if ((uint32_t)k < left) BKD_FOLD(B[k]);
+#pragma unroll
+            for (int k = 0; k < PF; ++k)
+                if ((uint32_t)(PF + k) < left) BKD_FOLD(A[k]);
+        } else {
+            for (uint32_t k = 0; k < rem; ++k) {
+                const u32x4 d = ld16<NT>(p + (int64_t)k * Gm::kStep);
+                BKD_FOLD(d);
+            }
+        }
+#undef BKD_FOLD
+
+        // Finish: lane Horner (x^32), lane tree (x^(128*2^s)), final x^32.
+        uint32_t v = mul_aux(lds, Gm::kX32Off, c0) ^ c1;
+        v = mul_aux(lds, Gm::kX32Off, v) ^ c2;
+        v = mul_aux(lds, Gm::kX32Off, v) ^ c3;
+#pragma unroll
+        for (int lv = 0; lv < Gm::kLevels; ++lv) {
+            const uint32_t other = (uint32_t)__shfl_xor((int)v, 1 << lv);
+            v = mul_aux(lds, Gm::kX32Off + 4096u * (uint32_t)(1 + lv), v) ^ other;
+        }
+        v = mul_aux(lds, Gm::kX32Off, v);
+        if (g == 0) out[i] = ~v;
+    }
+}
+
+// ---- synthetic input: little-endian splitmix64 stream ----
+__device__ __forceinline__ uint64_t splitmix_mix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ void fill_splitmix64_kernel(uint8_t* __restrict__ dst, uint64_t nbytes, uint64_t seed,
+                                       uint64_t first_word) {
+    const uint64_t nw = nbytes / 8;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t* d64 = reinterpret_cast<uint64_t*>(dst);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += stride)
+        d64[i] = splitmix_mix(seed + (first_word + i + 1) * 0x9E3779B97F4A7C15ull);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (nbytes & 7)) {
+        const uint64_t v = splitmix_mix(seed + (first_word + nw + 1) * 0x9E3779B97F4A7C15ull);
+        for (uint64_t k = 0; k < (nbytes & 7); ++k) dst[nw * 8 + k] = (uint8_t)(v >> (8 * k));
+    }
+}
+
+// ---- DigestManager framing helpers (one thread per entry; 32-byte headers) ----
+
+__device__ __forceinline__ uint32_t crc_bytes_serial(const uint32_t* btab, uint32_t reg, const uint8_t* p,
+                                                     uint32_t len) {
+    for (uint32_t k = 0; k < len; ++k) reg = btab[(reg ^ p[k]) & 0xffu] ^ (reg >> 8);
+    return reg;
+}
+
+__device__ __forceinline__ void put_be64(uint8_t* p, uint64_t v) {
+#pragma unroll
+    for (int k = 7; k >= 0; --k) {
+        p[k] = (uint8_t)v;
+        v >>= 8;
+    }
+}
+
+// Package step 1: header [ledgerId, entryId, LAC, length] BE into the frame
+// (DigestManager.java:146-149 / :172-175) and its CRC (= the payload's seed) into seeds[i].
+__global__ void package_header_kernel(const uint32_t* __restrict__ byte_table, int64_t ledger_id,
+                                      const int64_t* __restrict__ entry_ids, const int64_t* __restrict__ lacs,
+                                      const int64_t* __restrict__ length_fields, uint64_t n,
+                                      uint8_t* __restrict__ frames, uint64_t frame_stride,
+                                      uint32_t* __restrict__ seeds) {
+    __shared__ uint32_t bt[256];
+    for (int k = threadIdx.x; k < 256; k += blockDim.x) bt[k] = byte_table[k];
+    __syncthreads();
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint8_t h[32];
+    put_be64(h + 0, (uint64_t)ledger_id);
+    put_be64(h + 8, (uint64_t)entry_ids[i]);
+    put_be64(h + 16, (uint64_t)lacs[i]);
+    put_be64(h + 24, (uint64_t)length_fields[i]);
+    uint8_t* f = frames + i * frame_stride;
+    for (int k = 0; k < 32; ++k) f[k] = h[k];
+    seeds[i] = ~crc_bytes_serial(bt, 0xFFFFFFFFu, h, 32);
+}
+
+// Package step 3: the digest bytes after the header (CRC32CDigestManager.java:44-46: writeInt;
+// CRC32DigestManager.java:60-63: writeLong of the zero-extended value).
+__global__ void package_digest_kernel(const uint32_t* __restrict__ digests, uint64_t n, uint8_t* __restrict__ frames,
+                                      uint64_t frame_stride, uint32_t mac) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint8_t* f = frames + i * frame_stride + 32;
+    const uint32_t d = digests[i];
+    if (mac == 8) {
+        f[0] = f[1] = f[2] = f[3] = 0;
+        f += 4;
+    }
+    f[0] = (uint8_t)(d >> 24);
+    f[1] = (uint8_t)(d >> 16);
+    f[2] = (uint8_t)(d >> 8);
+    f[3] = (uint8_t)d;
+}
+
+// Verify step 1: CRC of the 32-byte header of each framed entry (DigestManager.java:236).
+__global__ void verify_header_kernel(const uint32_t* __restrict__ byte_table, const uint8_t* __restrict__ framed,
+                                     uint64_t size, const uint64_t* __restrict__ offsets,
+                                     const uint32_t* __restrict__ lengths, uint64_t n, uint32_t mac,
+                                     uint32_t* __restrict__ seeds, uint64_t* __restrict__ first_bad) {
+    __shared__ uint32_t bt[256];
+    for (int k = threadIdx.x; k < 256; k += blockDim.x) bt[k] = byte_table[k];
+    __syncthreads();
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) *first_bad = n;
+    if (i >= n) return;
+    const uint64_t o = offsets[i];
+    const uint32_t l = lengths[i];
+    uint32_t s = 0;
+    if (o <= size && (uint64_t)l <= size - o && l >= 32u + mac) s = ~crc_bytes_serial(bt, 0xFFFFFFFFu, framed + o, 32);
+    seeds[i] = s;
+}
+
+// Verify step 3: compare digest bytes and ids, per-entry status, first failing index
+// (DigestManager.java:241-281; BatchedReadOp.java:164-190 verified-prefix rule).
+__global__ void verify_finish_kernel(const uint8_t* __restrict__ framed, uint64_t size,
+                                     const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ lengths,
+                                     uint64_t n, uint32_t mac, int64_t ledger_id, int64_t first_entry_id,
+                                     int skip_entry_check, int32_t* __restrict__ status,
+                                     unsigned long long* __restrict__ first_bad) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t computed = (uint32_t)status[i];
+    const uint64_t o = offsets[i];
+    const uint32_t l = lengths[i];
+    int32_t st = 0;
+    if (o > size || (uint64_t)l > size - o || l < 32u + mac) {
+        st = 1;
+    } else {
+        const uint8_t* f = framed + o;
+        uint32_t stored;
+        bool hi_zero = true;
+        if (mac == 8) {
+            hi_zero = (f[32] | f[33] | f[34] | f[35]) == 0;
+            stored = ((uint32_t)f[36] << 24) | ((uint32_t)f[37] << 16) | ((uint32_t)f[38] << 8) | f[39];
+        } else {
+            stored = ((uint32_t)f[32] << 24) | ((uint32_t)f[33] << 16) | ((uint32_t)f[34] << 8) | f[35];
+        }
+        uint64_t lid = 0, eid = 0;
+        for (int k = 0; k < 8; ++k) {
+            lid = (lid << 8) | f[k];
+            eid = (eid << 8) | f[8 + k];
+        }
+        if (!hi_zero || stored != computed) st = 2;
+        else if ((int64_t)lid != ledger_id) st = 3;
+        else if (!skip_entry_check && (int64_t)eid != first_entry_id + (int64_t)i) st = 4;
+    }
+    status[i] = st;
+    if (st != 0) atomicMin(first_bad, (unsigned long long)i);
+}
+
+}  // namespace bkd

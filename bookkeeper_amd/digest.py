@@ -1,0 +1,228 @@
+"""Host-side mirror of BookKeeper's DigestManager family over the GPU engine.
+
+Reference: bookkeeper-server/src/main/java/org/apache/bookkeeper/proto/checksum/
+  DigestManager.java:46-401      framing, instantiate, package V2/V3, verify, LAC
+  CRC32CDigestManager.java:27-62 4-byte big-endian int digest via Crc32cIntChecksum
+  CRC32DigestManager.java:28-87  8-byte big-endian long digest (zero-extended CRC32)
+  DummyDigestManager.java:30-62  no digest
+HMAC (MacDigestManager) is HMAC-SHA1 arithmetic and outside this engine's scope.
+
+Per-entry methods keep the reference's two ``update`` calls (header, then payload). The batch
+methods (``package_batch`` / ``verify_batch``) are the new device path: one launch sequence
+frames or verifies thousands of device-resident entries.
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+import struct
+
+import numpy as np
+
+from . import checksum as _ck
+from ._native import (CRC32, CRC32C, VERIFY_DIGEST_MISMATCH, VERIFY_ENTRY_MISMATCH, VERIFY_LEDGER_MISMATCH,
+                      VERIFY_OK, VERIFY_TOO_SHORT, check, lib)
+
+METADATA_LENGTH = 32          # DigestManager.java:48
+LAC_METADATA_LENGTH = 16      # DigestManager.java:49
+MASTER_KEY_LENGTH = 20        # BookieProtocol.java:65
+CURRENT_PROTOCOL_VERSION = 2  # BookieProtocol.java:47
+ADDENTRY = 1                  # BookieProtocol.java:114
+FLAG_NONE = 0                 # BookieProtocol.java:188
+SMALL_ENTRY_SIZE_THRESHOLD = 16 * 1024  # BookieProtoEncoding.java:48
+INVALID_ENTRY_ID = -1         # LedgerHandle.INVALID_ENTRY_ID
+
+
+class DigestType(enum.Enum):  # DataFormats.proto:45-51
+    HMAC = 0
+    CRC32 = 1
+    CRC32C = 2
+    DUMMY = 3
+
+
+class BKDigestMatchException(Exception):
+    """BKException.BKDigestMatchException (DigestManager.java:234, 248, 260, 272, 280)."""
+
+    def __init__(self, reason: int = VERIFY_DIGEST_MISMATCH):
+        super().__init__({VERIFY_TOO_SHORT: "too short", VERIFY_DIGEST_MISMATCH: "digest mismatch",
+                          VERIFY_LEDGER_MISMATCH: "ledger id mismatch",
+                          VERIFY_ENTRY_MISMATCH: "entry id mismatch"}.get(reason, str(reason)))
+        self.reason = reason
+
+
+def packet_header_to_int(version: int, opcode: int, flags: int) -> int:
+    """BookieProtocol.PacketHeader.toInt (BookieProtocol.java:75-83)."""
+    if version == 0:
+        return opcode
+    return ((version & 0xFF) << 24) | ((opcode & 0xFF) << 16) | (flags & 0xFFFF)
+
+
+def _header(ledger_id: int, entry_id: int, lac: int, length: int) -> bytes:
+    # buf.writeLong x4, big-endian (DigestManager.java:146-149 / :172-175)
+    return struct.pack(">qqqq", ledger_id, entry_id, lac, length)
+
+
+class DigestManager:
+    algo: int | None = None
+    macCodeLength: int = 0
+
+    def __init__(self, ledgerId: int, useV2Protocol: bool = False):
+        self.ledgerId = int(ledgerId)
+        self.useV2Protocol = bool(useV2Protocol)
+        self._hash = _ck.GpuIntHash(self.algo) if self.algo is not None else None
+
+    # DigestManager.instantiate (DigestManager.java:88-102)
+    @staticmethod
+    def instantiate(ledgerId: int, passwd: bytes, digestType: DigestType, useV2Protocol: bool = False):
+        if digestType == DigestType.CRC32:
+            return CRC32DigestManager(ledgerId, useV2Protocol)
+        if digestType == DigestType.CRC32C:
+            return CRC32CDigestManager(ledgerId, useV2Protocol)
+        if digestType == DigestType.DUMMY:
+            return DummyDigestManager(ledgerId, useV2Protocol)
+        if digestType == DigestType.HMAC:
+            raise NotImplementedError("HMAC-SHA1 digests are outside the GPU CRC engine (SURVEY.md §2)")
+        raise ValueError(f"Unknown checksum type: {digestType}")
+
+    # ---- the two hooks subclasses define (DigestManager.java:56-76) ----
+    def update(self, digest: int, buf, offset: int, length: int) -> int:
+        return self._hash.resume(digest, buf, offset, length)
+
+    def digest_bytes(self, digest: int) -> bytes:
+        raise NotImplementedError
+
+    def isInt32Digest(self) -> bool:
+        raise NotImplementedError
+
+    # ---- packaging (DigestManager.java:117-181) ----
+    def computeDigestAndPackageForSending(self, entryId: int, lastAddConfirmed: int, length: int, data: bytes,
+                                          masterKey: bytes = b"\0" * MASTER_KEY_LENGTH,
+                                          flags: int = FLAG_NONE) -> bytes:
+        data = bytes(data)
+        hdr = _header(self.ledgerId, entryId, lastAddConfirmed, length)
+        digest = self.update(0, hdr, 0, METADATA_LENGTH)
+        digest = self.update(digest, data, 0, len(data))
+        dbytes = self.digest_bytes(digest)
+        if not self.useV2Protocol:  # V3: ByteBufList(header+digest, data)  (:169-181)
+            return hdr + dbytes + data
+        headers_size = 4 + MASTER_KEY_LENGTH + METADATA_LENGTH + self.macCodeLength  # :130-133
+        prefix = struct.pack(">ii", headers_size + len(data),
+                             packet_header_to_int(CURRENT_PROTOCOL_VERSION, ADDENTRY, flags))
+        return prefix + bytes(masterKey[:MASTER_KEY_LENGTH]) + hdr + dbytes + data  # :138-166
+
+    def computeDigestAndPackageForSendingLac(self, lac: int) -> bytes:  # :190-204
+        hdr = struct.pack(">qq", self.ledgerId, lac)
+        return hdr + self.digest_bytes(self.update(0, hdr, 0, LAC_METADATA_LENGTH))
+
+    # ---- verification (DigestManager.java:206-370) ----
+    def _verify(self, entryId: int, data: bytes, skipEntryIdCheck: bool) -> None:
+        data = bytes(data)
+        if METADATA_LENGTH + self.macCodeLength > len(data):
+            raise BKDigestMatchException(VERIFY_TOO_SHORT)
+        digest = self.update(0, data, 0, METADATA_LENGTH)
+        off = METADATA_LENGTH + self.macCodeLength
+        digest = self.update(digest, data, off, len(data) - off)
+        if self.digest_bytes(digest) != data[METADATA_LENGTH:METADATA_LENGTH + self.macCodeLength]:
+            raise BKDigestMatchException(VERIFY_DIGEST_MISMATCH)
+        actual_ledger, actual_entry = struct.unpack(">qq", data[:16])
+        if actual_ledger != self.ledgerId:
+            raise BKDigestMatchException(VERIFY_LEDGER_MISMATCH)
+        if not skipEntryIdCheck and actual_entry != entryId:
+            raise BKDigestMatchException(VERIFY_ENTRY_MISMATCH)
+
+    def verifyDigestAndReturnData(self, entryId: int, dataReceived: bytes) -> bytes:  # :333-338
+        self._verify(entryId, dataReceived, False)
+        return bytes(dataReceived)[METADATA_LENGTH + self.macCodeLength:]
+
+    def verifyDigestAndReturnLac(self, dataReceived: bytes) -> int:  # :285-323
+        data = bytes(dataReceived)
+        if LAC_METADATA_LENGTH + self.macCodeLength > len(data):
+            raise BKDigestMatchException(VERIFY_TOO_SHORT)
+        digest = self.update(0, data, 0, LAC_METADATA_LENGTH)
+        if self.digest_bytes(digest) != data[LAC_METADATA_LENGTH:LAC_METADATA_LENGTH + self.macCodeLength]:
+            raise BKDigestMatchException(VERIFY_DIGEST_MISMATCH)
+        ledger, lac = struct.unpack(">qq", data[:16])
+        if ledger != self.ledgerId:
+            raise BKDigestMatchException(VERIFY_LEDGER_MISMATCH)
+        return lac
+
+    # ---- batch device path (new) ----
+    def package_batch(self, entry_ids, lacs, length_fields, payload, offsets, lengths, frame_stride=None,
+                      stream=None):
+        """Frames n device-resident entries: returns (frames[n, frame_stride] uint8, digests int32[n]).
+        frames[i] = [32 B header][digest]; payload bytes stay where they are (ByteBufList(header, data))."""
+        import torch
+        n = offsets.numel()
+        stride = frame_stride or (METADATA_LENGTH + self.macCodeLength)
+        dev = payload.device
+        frames = torch.empty((n, stride), dtype=torch.uint8, device=dev)
+        digests = torch.empty(n, dtype=torch.int32, device=dev)
+        check(lib().bkd_digest_package_batch(
+            self.algo, self.ledgerId, _ck._dev_ptr(entry_ids, "entry_ids", torch.int64),
+            _ck._dev_ptr(lacs, "lacs", torch.int64), _ck._dev_ptr(length_fields, "length_fields", torch.int64),
+            _ck._dev_ptr(payload, "payload"), payload.numel() * payload.element_size(),
+            _ck._dev_ptr(offsets, "offsets", torch.int64), _ck._dev_ptr(lengths, "lengths", torch.int32), n,
+            _ck._dev_ptr(frames, "frames"), stride, _ck._dev_ptr(digests, "digests"),
+            _ck._stream_ptr(stream, payload)))
+        return frames, digests
+
+    def verify_batch(self, framed, offsets, lengths, first_entry_id: int, skip_entry_check: bool = False,
+                     stream=None):
+        """Verifies n framed entries on the device; returns (status int32[n], first_bad int64[1])
+        with BatchedReadOp's verified-prefix rule: entries [0, first_bad) verified."""
+        import torch
+        n = offsets.numel()
+        dev = framed.device
+        status = torch.empty(n, dtype=torch.int32, device=dev)
+        first_bad = torch.empty(1, dtype=torch.int64, device=dev)
+        check(lib().bkd_digest_verify_batch(
+            self.algo, self.ledgerId, first_entry_id, int(skip_entry_check), _ck._dev_ptr(framed, "framed"),
+            framed.numel() * framed.element_size(), _ck._dev_ptr(offsets, "offsets", torch.int64),
+            _ck._dev_ptr(lengths, "lengths", torch.int32), n, _ck._dev_ptr(status, "status"),
+            _ck._dev_ptr(first_bad, "first_bad"), _ck._stream_ptr(stream, framed)))
+        return status, first_bad
+
+
+class CRC32CDigestManager(DigestManager):
+    """CRC32CDigestManager.java:27-62."""
+    algo = CRC32C
+    macCodeLength = 4
+
+    def digest_bytes(self, digest: int) -> bytes:  # buf.writeInt(digest)  (:44-46)
+        return struct.pack(">i", _ck.to_java_int(digest))
+
+    def isInt32Digest(self) -> bool:
+        return True
+
+
+class CRC32DigestManager(DigestManager):
+    """CRC32DigestManager.java:28-87: the CRC is carried as an int through update() and written as
+    writeLong(crcValue & 0xffffffffL) (:60-63, DirectMemoryCRC32Digest.java:39-43)."""
+    algo = CRC32
+    macCodeLength = 8
+
+    def digest_bytes(self, digest: int) -> bytes:
+        return struct.pack(">Q", digest & 0xFFFFFFFF)
+
+    def isInt32Digest(self) -> bool:
+        return False
+
+
+class DummyDigestManager(DigestManager):
+    """DummyDigestManager.java:30-62: no digest bytes, update is a no-op."""
+    algo = None
+    macCodeLength = 0
+
+    def update(self, digest, buf, offset, length):
+        return 0
+
+    def digest_bytes(self, digest: int) -> bytes:
+        return b""
+
+    def isInt32Digest(self) -> bool:
+        return True
+
+    def package_batch(self, *a, **k):
+        raise NotImplementedError("DUMMY digests need no device work")
+
+    verify_batch = package_batch

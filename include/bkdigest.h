@@ -1,0 +1,158 @@
+/*
+ * bkdigest — MI355X-native ledger-entry digest engine (CRC32C / CRC32) for Apache BookKeeper.
+ *
+ * The drop-in boundary: a C-ABI shared library (bookkeeper_amd/libbkdigest.so) with plain
+ * pointers and sizes. Every entry point names the reference interface it replaces
+ * (paths relative to /root/reference; $CN = circe-checksum/src/main/circe,
+ * $CJ = circe-checksum/src/main/java/com/scurrilous/circe,
+ * $BK = bookkeeper-server/src/main/java/org/apache/bookkeeper).
+ *
+ * Semantics shared by every CRC entry point (identical to the reference):
+ *   - `current` / seeds are FINALIZED CRCs: resume(prev, x) = ~raw(~prev, x)
+ *     ($CN/cpp/crc32c_sse42.cpp:187,213; $CJ/crc/AbstractIntCrc.java:55-57);
+ *   - calculate(x) == resume(0, x) ($CJ/checksum/JniIntHash.java:40-42);
+ *   - a zero-length entry returns its seed unchanged ($CN/cpp/crc32c_sse42.cpp:211-213);
+ *   - the value is the u32 bit pattern of the Java `int` the reference returns.
+ * Algorithms: BKD_CRC32C = CRC-32C (Castagnoli, reflected 0x82F63B78, $CN/cpp/crc32c_sse42.cpp:85),
+ *             BKD_CRC32  = CRC-32 (ISO-HDLC, reflected 0xEDB88320, java.util.zip.CRC32 as used by
+ *                          $BK/proto/checksum/CRC32DigestManager.java:28-87).
+ *
+ * Errors are return codes only (the reference native never throws, circe-checksum/pom.xml:87);
+ * a human-readable message for the calling thread is available from bkd_last_error().
+ * All entry points are thread-safe. Device-resident batch calls are asynchronous on the
+ * caller's HIP stream (hipStream_t passed as void*, NULL = the null stream); buffers are
+ * borrowed only until the stream reaches the end of the call's work.
+ * There is no CPU compute path: without a usable GPU the calls return BKD_ERR_NO_DEVICE
+ * and the caller keeps its own CPU provider ($CJ/checksum/Crc32cIntChecksum.java:28-36 chain).
+ */
+#ifndef BKDIGEST_H_
+#define BKDIGEST_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BKD_ABI_VERSION 1
+
+/* return codes */
+#define BKD_OK 0
+#define BKD_ERR_INVALID_ARG (-1)
+#define BKD_ERR_NO_DEVICE (-2)
+#define BKD_ERR_HIP (-3)
+#define BKD_ERR_BOUNDS (-4)
+#define BKD_ERR_NOMEM (-5)
+
+/* algorithms */
+#define BKD_CRC32C 0
+#define BKD_CRC32 1
+
+/* verify status codes (one per entry), mirroring DigestManager.verifyDigest's failure modes
+ * ($BK/proto/checksum/DigestManager.java:226-283) */
+#define BKD_VERIFY_OK 0
+#define BKD_VERIFY_TOO_SHORT 1      /* :229-235 (METADATA_LENGTH + macCodeLength) > readableBytes */
+#define BKD_VERIFY_DIGEST_MISMATCH 2 /* :241-261 */
+#define BKD_VERIFY_LEDGER_MISMATCH 3 /* :267-273 */
+#define BKD_VERIFY_ENTRY_MISMATCH 4  /* :275-281 */
+
+int bkd_abi_version(void);
+
+/* Number of visible HIP devices (0 when none). Replaces the capability probe
+ * Sse42Crc32C.isSupported() -> nativeSupported() ($CJ/crc/Sse42Crc32C.java:31-47,
+ * $CN/cpp/crc32c_sse42_jni.cpp:20-24). */
+int bkd_device_count(void);
+
+/* Uploads the CRC fold tables to `device` (idempotent, thread-safe). Replaces the
+ * allocConfig chunk/shift-table construction ($CN/cpp/crc32c_sse42_jni.cpp:50-72,
+ * $CN/cpp/crc32c_sse42.cpp:74-90). Optional: every call below initialises lazily. */
+int bkd_init(int device);
+
+/* Message describing the last failure on the calling thread ("" if none). */
+const char* bkd_last_error(void);
+
+/* ---- device-resident batches: THE HOT PATH ---------------------------------------------
+ * One CRC per entry, all entries in one launch. Entry i is the byte range
+ *   uniform:  d_base + i*stride, entry_len bytes
+ *   indexed:  d_base + d_offsets[i], d_lengths[i] bytes (any alignment, any order)
+ * seeded with d_seeds[i] (finalized CRC) or, when d_seeds is NULL, with seed_all.
+ * d_out[i] receives the finalized CRC. All pointers are device pointers of the current
+ * HIP device. Replaces N calls of Sse42Crc32C.resume(int,long,long) -> nativeUnsafe
+ * ($CJ/crc/Sse42Crc32C.java:105-107, $CN/cpp/crc32c_sse42_jni.cpp:44-48) which the
+ * reference makes once per entry from DigestManager.update ($BK/proto/checksum/DigestManager.java:62-72).
+ * The indexed form checks offset+length <= base_size for every entry on the device and returns
+ * BKD_ERR_BOUNDS from the NEXT synchronous call on this stream if any entry was out of range
+ * (those entries get out = 0 and are not read). */
+int bkd_crc_batch_uniform(int algo, const void* d_base, uint64_t stride, uint32_t entry_len, uint64_t n,
+                          const uint32_t* d_seeds, uint32_t seed_all, uint32_t* d_out, void* stream);
+
+int bkd_crc_batch(int algo, const void* d_base, uint64_t base_size, const uint64_t* d_offsets,
+                  const uint32_t* d_lengths, uint64_t n, const uint32_t* d_seeds, uint32_t seed_all,
+                  uint32_t* d_out, void* stream);
+
+/* Waits for `stream` and reports any bounds violation recorded by earlier indexed batches. */
+int bkd_stream_sync(void* stream);
+
+/* ---- host-resident batches (the end-to-end path: Netty buffers in, digests out) -------
+ * Synchronous. Copies the payload through pinned staging buffers with hipMemcpyAsync
+ * (double-buffered H2D -> kernel -> D2H). Same semantics as bkd_crc_batch. */
+int bkd_crc_batch_host(int algo, const void* h_base, uint64_t base_size, const uint64_t* h_offsets,
+                       const uint32_t* h_lengths, uint64_t n, const uint32_t* h_seeds, uint32_t seed_all,
+                       uint32_t* h_out);
+
+/* ---- per-call drop-in (IntHash.resume) ---------------------------------------------------
+ * resume(current, ptr, len) for ONE buffer (host or device pointer), synchronous.
+ * Replaces Sse42Crc32C.nativeUnsafe / nativeArray / nativeDirectBuffer
+ * ($CN/cpp/crc32c_sse42_jni.cpp:26-48) and IntHash.resume ($CJ/checksum/IntHash.java:28-32).
+ * Latency-bound by design (one launch per call); batch callers use bkd_crc_batch. */
+int bkd_resume(int algo, uint32_t current, const void* ptr, uint64_t len, uint32_t* out);
+
+/* ---- DigestManager batch framing (§8f rows 1-2) --------------------------------------
+ * Package: for entry i with payload d_payload + d_offsets[i], d_lengths[i] bytes, write the
+ * 32-byte big-endian header [ledger_id, entry_ids[i], lacs[i], lengths_field[i]]
+ * ($BK/proto/checksum/DigestManager.java:146-149) followed by the digest
+ * (CRC32C: 4 B BE int, CRC32CDigestManager.java:44-46; CRC32: 8 B BE long zero-extended,
+ * CRC32DigestManager.java:60-63) into d_frames + i*frame_stride (frame_stride >= 32 + mac).
+ * digest = update(update(0, header), payload) (DigestManager.java:152-153, :177-178).
+ * Device pointers; asynchronous on `stream`. */
+int bkd_digest_package_batch(int algo, int64_t ledger_id, const int64_t* d_entry_ids, const int64_t* d_lacs,
+                             const int64_t* d_length_fields, const void* d_payload, uint64_t payload_size,
+                             const uint64_t* d_offsets, const uint32_t* d_lengths, uint64_t n,
+                             void* d_frames, uint64_t frame_stride, uint32_t* d_digests, void* stream);
+
+/* Verify: entry i is a framed buffer [32 B header][mac][payload] at d_framed + d_offsets[i],
+ * d_lengths[i] bytes. Writes a BKD_VERIFY_* code per entry to d_status and the index of the first
+ * failing entry (n if none) to *d_first_bad — the verified-prefix rule of BatchedReadOp
+ * ($BK/client/BatchedReadOp.java:164-190). expected entry id for entry i = first_entry_id + i
+ * (DigestManager.verifyDigestAndReturnData(entryId, buf), :333-338); skip_entry_check mirrors
+ * verifyDigest(buf) with skipEntryIdCheck (:206-208). Device pointers; asynchronous. */
+int bkd_digest_verify_batch(int algo, int64_t ledger_id, int64_t first_entry_id, int skip_entry_check,
+                            const void* d_framed, uint64_t framed_size, const uint64_t* d_offsets,
+                            const uint32_t* d_lengths, uint64_t n, int32_t* d_status, uint64_t* d_first_bad,
+                            void* stream);
+
+/* ---- synthetic input + test helpers --------------------------------------------------- */
+
+/* Fills nbytes of device memory with the little-endian splitmix64 stream
+ * word_i = mix(seed + (first_word + i + 1) * 0x9E3779B97F4A7C15) (SURVEY.md §8d input definition). */
+int bkd_fill_splitmix64(void* d_dst, uint64_t nbytes, uint64_t seed, uint64_t first_word, void* stream);
+
+/* Host-only (no GPU needed): the compact fold-table image the kernels load into LDS for
+ * `algo` and a group width of `lanes` (4, 8, 16, 32 or 64); returns words written or <0.
+ * Layout documented in DESIGN.md §3. */
+int64_t bkd_host_tables(int algo, int lanes, uint32_t* out, uint64_t out_words);
+
+/* Host-only: GF(2) product a*b mod P in the reflected representation, and x^(8*nbytes) mod P. */
+uint32_t bkd_host_gf_mul(int algo, uint32_t a, uint32_t b);
+uint32_t bkd_host_xpow8n(int algo, uint64_t nbytes);
+
+/* Tuning: lanes per entry group (0 = automatic, else 4/8/16/32/64); prefetch is fixed at build. */
+int bkd_set_group_lanes(int lanes);
+int bkd_get_group_lanes(int algo, uint64_t mean_len);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BKDIGEST_H_ */

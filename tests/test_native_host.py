@@ -1,0 +1,83 @@
+"""CPU: the C-ABI library loads and exports every symbol include/bkdigest.h declares; its
+host-side operator tables are right; and the kernel's decomposition (modelled in Python
+with the library's own tables) reproduces the oracle bit-exactly. No GPU compute here."""
+import ctypes
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+from bookkeeper_amd import _native
+from bookkeeper_amd import checksum as ck
+from bookkeeper_amd.build import LIB
+from kernel_model import KernelModel
+
+
+def test_library_exports_every_declared_symbol():
+    L = _native.lib()
+    declared = _native.declared_functions()
+    assert len(declared) >= 15
+    for name in declared:
+        assert hasattr(L, name), name
+    assert set(declared) == set(_native.PROTOTYPES)
+    dyn = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True).stdout
+    exported = {line.split()[-1] for line in dyn.splitlines() if " T " in line}
+    assert set(declared) <= exported
+    assert L.bkd_abi_version() == 1
+
+
+def test_library_contains_gfx950_code():
+    blob = open(LIB, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob  # offload bundle entry id for the gfx950 code object
+
+
+def test_no_device_is_an_error_not_a_fallback():
+    if _native.device_count() > 0:
+        pytest.skip("a device is visible")
+    out = ctypes.c_uint32(0)
+    rc = _native.lib().bkd_resume(0, 0, b"123456789", 9, ctypes.byref(out))
+    assert rc == -2  # BKD_ERR_NO_DEVICE: no silent CPU path
+    with pytest.raises(_native.BkdError):
+        ck.GpuIntHash().calculate(b"123456789")
+
+
+@pytest.mark.parametrize("algo", [0, 1])
+def test_host_tables_against_oracle(algo):
+    L = _native.lib()
+    for lanes in (4, 8, 16, 32, 64):
+        t = ck.host_tables(algo, lanes)
+        assert t.size == (2 + int(np.log2(lanes))) * 1024 + 256
+        assert (t[-256:] == oracle.table(algo)).all()  # ReflectedIntCrc.java:30-35
+        # main operator C = x^(128*lanes): every byte table entry is (b << 8t) * C mod P
+        C = oracle.xpow8n(algo, 16 * lanes)
+        for tb in range(4):
+            for b in (0, 1, 0x80, 0xFF, 0x5A):
+                assert t[tb * 256 + b] == oracle.gf_mul(algo, b << (8 * tb), C)
+    rng = np.random.default_rng(algo)
+    for _ in range(50):
+        a, b = (int(x) for x in rng.integers(0, 2**32, 2))
+        assert L.bkd_host_gf_mul(algo, a, b) == oracle.gf_mul(algo, a, b)
+    for n in (0, 1, 4, 16, 4096, 65536, 10**9):
+        assert L.bkd_host_xpow8n(algo, n) == oracle.xpow8n(algo, n)
+
+
+@pytest.mark.parametrize("algo", [0, 1])
+@pytest.mark.parametrize("lanes", [4, 8, 16, 64])
+def test_kernel_decomposition_model(algo, lanes):
+    model = KernelModel(ck.host_tables(algo, lanes), lanes)
+    rng = np.random.default_rng(lanes + algo)
+    for n in [0, 1, 3, 4, 5, 15, 16, 17, 31, 32, 33, 64, 100, 16 * lanes - 1, 16 * lanes, 16 * lanes + 1, 2500]:
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        for seed in (0, int(rng.integers(0, 2**32))):
+            assert model.crc(d, seed) == oracle.resume(algo, seed, d), (n, seed)
+
+
+def test_group_lane_policy():
+    L = _native.lib()
+    assert ck.set_group_lanes(8) is None
+    assert L.bkd_get_group_lanes(0, 4096) == 8
+    ck.set_group_lanes(0)
+    assert L.bkd_get_group_lanes(0, 4096) in (4, 8, 16)
+    with pytest.raises(_native.BkdError):
+        ck.set_group_lanes(3)
