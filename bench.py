@@ -185,7 +185,7 @@ def main() -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max = float(t.item())
 
-    total_payload = payload_bytes * world
+    total_payload = payload_bytes * world * args.steps  # every rank processes its batch once per step
     value = total_payload / elapsed_max / GIB
     achieved_gbs = algo_bytes / avg_kernel_s / 1e9
     result = {
@@ -203,6 +203,7 @@ def main() -> None:
         "data": "synthetic (device-generated splitmix64, seed 42)",
         "config": dict(workload, parallelism=f"shard{world} (independent entries, no collective)",
                        lanes=ck.lib().bkd_get_group_lanes(algo, payload_bytes // max(1, n))),
+        # payload GB/s over the aggregate HBM peak of the GPUs used (the metric's "% HBM peak")
         "hbm_peak_frac": round(value * GIB / 1e9 / (HBM_PEAK_GBS * world), 4),
         "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic(args.config),

@@ -108,8 +108,16 @@ int auto_lanes(uint64_t mean_len) {
     return 32;
 }
 
-constexpr int kPF = 4;
-constexpr bool kNT = false;
+// Loads in flight per lane (register double buffer depth) and load cache policy; build-time
+// knobs so variants can be A/B-timed in one process (tools/tune.py).
+#ifndef BKD_PF
+#define BKD_PF 2
+#endif
+#ifndef BKD_NT
+#define BKD_NT 1
+#endif
+constexpr int kPF = BKD_PF;
+constexpr bool kNT = BKD_NT != 0;
 
 template <int G, class Src>
 int launch_groups(DeviceState& ds, int algo, const uint8_t* base, const Src& src, uint64_t n, uint32_t* out,

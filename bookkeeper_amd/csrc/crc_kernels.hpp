@@ -210,14 +210,18 @@ __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __res
         } else {
             w = u32x4{0u, 0u, 0u, 0u};
         }
+        const uint32_t r0 = ~seed;
         if (a < s + 4 && a + 16 > s) {
-            const uint32_t r0 = ~seed;
             const int64_t d = s - a;
             w.x ^= place_seed(r0, d);
             w.y ^= place_seed(r0, d - 4);
             w.z ^= place_seed(r0, d - 8);
             w.w ^= place_seed(r0, d - 12);
         }
+        // When the entry starts in the last 3 bytes of step 0's window, the tail of the seed
+        // image spills into dword 0 of lane 0 at step 1; fx carries it into that first fold.
+        uint32_t fx = 0u;
+        if (a + Gm::kStep < s + 4) fx = place_seed(r0, s - (a + Gm::kStep));
         uint32_t c0 = w.x, c1 = w.y, c2 = w.z, c3 = w.w;
 
         // Steps 1..J-1 with PF loads in flight per lane. The steady-state loop issues its
@@ -225,6 +229,14 @@ __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __res
         // early vmcnt(0)); only the < PF-step tail is handled with guarded code.
         const uint8_t* p = base + a + Gm::kStep;
         const uint32_t rem = J - 1u;
+#define BKD_FOLD0(d)                                     \
+    do {                                                 \
+        c0 = mul_main(lds, c0, lanereg) ^ (d).x ^ fx;    \
+        fx = 0u;                                         \
+        c1 = mul_main(lds, c1, lanereg) ^ (d).y;         \
+        c2 = mul_main(lds, c2, lanereg) ^ (d).z;         \
+        c3 = mul_main(lds, c3, lanereg) ^ (d).w;         \
+    } while (0)
 #define BKD_FOLD(d)                                  \
     do {                                             \
         c0 = mul_main(lds, c0, lanereg) ^ (d).x;     \
@@ -242,8 +254,9 @@ __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __res
             while (left >= 2u * PF) {
 #pragma unroll
                 for (int k = 0; k < PF; ++k) B[k] = ld16<NT>(p + (int64_t)k * Gm::kStep);
+                BKD_FOLD0(A[0]);
 #pragma unroll
-                for (int k = 0; k < PF; ++k) BKD_FOLD(A[k]);
+                for (int k = 1; k < PF; ++k) BKD_FOLD(A[k]);
 #pragma unroll
                 for (int k = 0; k < PF; ++k) A[k] = ld16<NT>(p + (int64_t)(PF + k) * Gm::kStep);
 #pragma unroll
@@ -255,8 +268,9 @@ __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __res
 #pragma unroll
             for (int k = 0; k < PF; ++k)
                 if ((uint32_t)k < left) B[k] = ld16<NT>(p + (int64_t)k * Gm::kStep);
+            BKD_FOLD0(A[0]);
 #pragma unroll
-            for (int k = 0; k < PF; ++k) BKD_FOLD(A[k]);
+            for (int k = 1; k < PF; ++k) BKD_FOLD(A[k]);
 #pragma unroll
             for (int k = 0; k < PF; ++k)
                 if ((uint32_t)(PF + k) < left) A[k] = ld16<NT>(p + (int64_t)(PF + k) * Gm::kStep);
@@ -269,10 +283,11 @@ __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __res
         } else {
             for (uint32_t k = 0; k < rem; ++k) {
                 const u32x4 d = ld16<NT>(p + (int64_t)k * Gm::kStep);
-                BKD_FOLD(d);
+                BKD_FOLD0(d);
             }
         }
 #undef BKD_FOLD
+#undef BKD_FOLD0
 
         // Finish: lane Horner (x^32), lane tree (x^(128*2^s)), final x^32.
         uint32_t v = mul_aux(lds, Gm::kX32Off, c0) ^ c1;

@@ -31,14 +31,39 @@ class KernelModel:
             return (~r) & 0xFFFFFFFF
         G, step = self.G, 16 * self.G
         J = (n + step - 1) // step
-        W = J * step
-        pad = W - n
-        # virtual window: zeros in front of the entry, then the entry
-        win = bytearray(pad) + bytearray(data)
+        buf = bytes(data)
+        s, e = 0, n                      # entry byte range (relative)
+        wstart = e - J * step
         r0 = (~seed) & 0xFFFFFFFF
-        for k in range(4):  # fold the init register into the entry's first 4 bytes
-            win[pad + k] ^= (r0 >> (8 * k)) & 0xFF
-        words = np.frombuffer(bytes(win), dtype="<u4").reshape(J, G, 4)
+
+        def place(d):                     # place_seed() in crc_kernels.hpp
+            if 0 <= d <= 3:
+                return (r0 << (8 * d)) & 0xFFFFFFFF
+            if -3 <= d < 0:
+                return r0 >> (8 * -d)
+            return 0
+
+        def load16(addr):                 # addr >= s and addr + 16 <= e, like the kernel
+            return [int.from_bytes(buf[addr + 4 * k: addr + 4 * k + 4], "little") for k in range(4)]
+
+        words = np.zeros((J, G, 4), dtype=np.uint64)
+        for g in range(G):
+            a = wstart + 16 * g
+            if a >= s:
+                w = load16(a)
+            elif a + 16 > s:              # straddling lane: load at s, shift left by s - a bytes
+                v = int.from_bytes(buf[s:s + 16], "little") << (8 * (s - a))
+                w = [(v >> (32 * k)) & 0xFFFFFFFF for k in range(4)]
+            else:
+                w = [0, 0, 0, 0]
+            if a < s + 4 and a + 16 > s:
+                w = [w[k] ^ place(s - a - 4 * k) for k in range(4)]
+            words[0, g] = w
+            for j in range(1, J):
+                words[j, g] = load16(a + j * step)
+        fx = place(s - (wstart + step)) if wstart + step < s + 4 else 0
+        if J > 1:
+            words[1, 0, 0] ^= fx
         lane_vals = []
         for g in range(G):
             acc = [int(words[0, g, k]) for k in range(4)]
