@@ -30,7 +30,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.
 METRIC = "GiB/s CRC32C over batched 4 KiB ledger entries (device-resident); % HBM peak"
 
 
-def zipf_index(n: int, seed: int = 43, s: float = 1.1, kmax: int = 1024):
+def zipf_index(n: int, seed: int = 43, s: float = 1.1, kmax: int = 1024, align: int = 1):
     """k ~ Zipf(s) on {1..kmax} by inverse CDF over a splitmix64 stream,
     len = max(64, 64k - (r & 63)); entries packed back to back (unaligned starts)."""
     words = np.frombuffer(_splitmix_words(2 * n, seed), dtype=np.uint64)
@@ -42,6 +42,8 @@ def zipf_index(n: int, seed: int = 43, s: float = 1.1, kmax: int = 1024):
     kk = np.searchsorted(cdf, u, side="right") + 1
     kk = np.minimum(kk, kmax)
     lengths = np.maximum(64, 64 * kk - (r & np.uint64(63)).astype(np.int64)).astype(np.int64)
+    if align > 1:  # diagnostic only: round lengths up so every entry starts on an `align` boundary
+        lengths = (lengths + align - 1) // align * align
     offsets = np.zeros(n, dtype=np.int64)
     np.cumsum(lengths[:-1], out=offsets[1:])
     return offsets, lengths
@@ -101,12 +103,14 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="uniform4k", choices=["uniform4k", "shard8m", "zipf"])
+    ap.add_argument("--config", default="uniform4k", choices=["uniform4k", "shard8m", "zipf", "indexed4k"])
     ap.add_argument("--algo", default="crc32c", choices=["crc32c", "crc32"])
     ap.add_argument("--entries", type=int, default=0, help="entries per GPU (default by config)")
     ap.add_argument("--lanes", type=int, default=0, help="force lanes per entry group (0 = auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--zipf-align", type=int, default=1, help="diagnostic: align Zipf entries")
+    ap.add_argument("--plan-mode", type=int, default=0, help="0 auto, 1 direct, 2 chunked plan")
     args = ap.parse_args()
 
     import torch
@@ -126,6 +130,7 @@ def main() -> None:
         dist.init_process_group("nccl", device_id=dev)
     algo = ck.CRC32C if args.algo == "crc32c" else ck.CRC32
     ck.set_group_lanes(args.lanes)
+    ck.set_plan_mode(args.plan_mode)
 
     stream = torch.cuda.current_stream(dev)
     if args.config in ("uniform4k", "shard8m"):
@@ -144,7 +149,11 @@ def main() -> None:
                     "entries_per_gpu": n, "entry_bytes": entry_len}
     else:
         n = args.entries or (1 << 20)
-        offs, lens = zipf_index(n)
+        if args.config == "indexed4k":  # diagnostic: the uniform layout through the indexed (plan) path
+            offs = np.arange(n, dtype=np.int64) * 4096
+            lens = np.full(n, 4096, dtype=np.int64)
+        else:
+            offs, lens = zipf_index(n, align=args.zipf_align)
         total = int(offs[-1] + lens[-1])
         base = torch.empty(total, dtype=torch.uint8, device=dev)
         ck.fill_splitmix64(base, 42, first_word=0)
@@ -210,7 +219,7 @@ def main() -> None:
                      "kernel": "crc_groups_kernel", "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
                      "algorithmic_bytes_per_launch": algo_bytes},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config != "zipf":
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in ("uniform4k", "shard8m"):
         # cpu_baseline leg: the reference timed on the host cores over a bounded sample; its
         # digests for that sample double as a parity spot check of the GPU output.
         m = min(n, 65536)

@@ -14,7 +14,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libbkdigest.so")
 SOURCES = [os.path.join(CSRC, "bkdigest.hip")]
-DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("crc_kernels.hpp", "crc_tables.hpp")] + [
+DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("crc_kernels.hpp", "crc_tables.hpp", "plan_kernels.hpp")] + [
     os.path.join(ROOT, "include", "bkdigest.h")]
 ARCH = os.environ.get("BKD_OFFLOAD_ARCH", "gfx950")
 

@@ -215,8 +215,17 @@ def set_group_lanes(lanes: int) -> None:
     check(lib().bkd_set_group_lanes(lanes))
 
 
+def set_plan_mode(mode: int) -> None:
+    """0 = auto, 1 = one entry per lane group, 2 = chunked plan (indexed batches)."""
+    check(lib().bkd_set_plan_mode(mode))
+
+
+def set_plan_geometry(lanes: int = 8, steps_per_chunk: int = 32, merge_bytes: int = 16) -> None:
+    check(lib().bkd_set_plan_geometry(lanes, steps_per_chunk, merge_bytes))
+
+
 def host_tables(algo: int, lanes: int) -> np.ndarray:
-    n = (2 + int(np.log2(lanes))) * 1024 + 256
+    n = (2 + int(np.log2(lanes))) * 1024 + 256 + 2048
     out = np.zeros(n, dtype=np.uint32)
     check(lib().bkd_host_tables(algo, lanes, ctypes.c_void_p(out.ctypes.data), n))
     return out

@@ -9,12 +9,14 @@
 
 #include <algorithm>
 #include <atomic>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
 
 #include "../../include/bkdigest.h"
 #include "crc_kernels.hpp"
+#include "plan_kernels.hpp"
 #include "crc_tables.hpp"
 
 namespace {
@@ -46,11 +48,21 @@ struct DeviceState {
     int cus = 0;
     uint32_t* tables[2][5] = {};  // [algo][lane choice] compact operator images
     uint32_t* err = nullptr;      // sticky bounds-violation flag for indexed batches
+    std::map<uint64_t, uint32_t*> xtab;  // (algo, CH) -> x^(8*CH) operator for the plan's combine
 };
 
 std::mutex g_mu;
 DeviceState g_dev[kMaxDevices];
 std::atomic<int> g_forced_lanes{0};
+std::atomic<int> g_plan_mode{0};  // 0 auto, 1 direct (one entry per group), 2 chunked plan
+
+// Chunked plan geometry (bkd_set_plan_geometry): lanes per group, steps per full chunk
+// (CH = 16 * lanes * jc bytes) and the head-merge threshold in bytes.
+std::atomic<int> g_plan_lanes{8};
+std::atomic<int> g_plan_jc{32};
+std::atomic<int> g_plan_merge{16};
+// Indexed batches whose base buffer is at most this size skip the plan (latency over balance).
+constexpr uint64_t kDirectMaxBytes = 256u << 10;
 
 int current_device(int* dev) {
     int count = 0;
@@ -79,10 +91,33 @@ int init_device_locked(int dev) {
             BKD_HIP(hipMemcpy(ds.tables[algo][k], img.data(), img.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
         }
     }
+    // stream-ordered scratch for the plan: keep freed blocks in the pool between calls
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+        uint64_t thr = UINT64_MAX;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+    }
     BKD_HIP(hipMalloc(&ds.err, sizeof(uint32_t)));
     BKD_HIP(hipMemset(ds.err, 0, sizeof(uint32_t)));
     BKD_HIP(hipSetDevice(prev));
     ds.ready = true;
+    return BKD_OK;
+}
+
+// x^(8*ch) operator tables for the plan's combine, built once per (algo, ch) and device.
+int xtab_for(DeviceState& ds, int algo, uint32_t ch, const uint32_t** out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    const uint64_t key = ((uint64_t)algo << 32) | ch;
+    auto it = ds.xtab.find(key);
+    if (it == ds.xtab.end()) {
+        std::vector<uint32_t> xt(1024);
+        bkd::gf2::operator_tables(algo, bkd::gf2::xpow(algo, 8ull * ch), xt.data());
+        uint32_t* d = nullptr;
+        BKD_HIP(hipMalloc(&d, xt.size() * sizeof(uint32_t)));
+        BKD_HIP(hipMemcpy(d, xt.data(), xt.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        it = ds.xtab.emplace(key, d).first;
+    }
+    *out = it->second;
     return BKD_OK;
 }
 
@@ -120,30 +155,108 @@ constexpr int kPF = BKD_PF;
 constexpr bool kNT = BKD_NT != 0;
 
 template <int G, class Src>
-int launch_groups(DeviceState& ds, int algo, const uint8_t* base, const Src& src, uint64_t n, uint32_t* out,
+int launch_groups(DeviceState& ds, int algo, const uint8_t* base, const Src& src, uint64_t host_count,
                   hipStream_t stream) {
-    if (n == 0) return BKD_OK;
+    if (host_count == 0) return BKD_OK;
     const uint64_t groups_per_block = bkd::kBlock / G;
-    uint64_t blocks = (n + groups_per_block - 1) / groups_per_block;
+    uint64_t blocks = (host_count + groups_per_block - 1) / groups_per_block;
     blocks = std::min<uint64_t>(blocks, (uint64_t)ds.cus);
     const uint32_t* tab = ds.tables[algo][lane_index(G)];
     hipLaunchKernelGGL((bkd::crc_groups_kernel<G, kPF, kNT, Src>), dim3((unsigned)blocks), dim3(bkd::kBlock), 0,
-                       stream, base, src, n, tab, out, ds.err);
+                       stream, base, src, tab, ds.err);
     BKD_HIP(hipGetLastError());
     return BKD_OK;
 }
 
+// host_count: an upper bound of src.count() used only to size the grid.
 template <class Src>
-int dispatch_lanes(DeviceState& ds, int lanes, int algo, const uint8_t* base, const Src& src, uint64_t n,
-                   uint32_t* out, hipStream_t stream) {
+int dispatch_lanes(DeviceState& ds, int lanes, int algo, const uint8_t* base, const Src& src, uint64_t host_count,
+                   hipStream_t stream) {
     switch (lanes) {
-        case 4: return launch_groups<4>(ds, algo, base, src, n, out, stream);
-        case 8: return launch_groups<8>(ds, algo, base, src, n, out, stream);
-        case 16: return launch_groups<16>(ds, algo, base, src, n, out, stream);
-        case 32: return launch_groups<32>(ds, algo, base, src, n, out, stream);
-        case 64: return launch_groups<64>(ds, algo, base, src, n, out, stream);
+        case 4: return launch_groups<4>(ds, algo, base, src, host_count, stream);
+        case 8: return launch_groups<8>(ds, algo, base, src, host_count, stream);
+        case 16: return launch_groups<16>(ds, algo, base, src, host_count, stream);
+        case 32: return launch_groups<32>(ds, algo, base, src, host_count, stream);
+        case 64: return launch_groups<64>(ds, algo, base, src, host_count, stream);
         default: return fail(BKD_ERR_INVALID_ARG, "lanes must be 4, 8, 16, 32 or 64");
     }
+}
+
+template <int G>
+void launch_plan_chunks(const uint8_t* base, const bkd::PlanDesc* descs, const uint32_t* count, const uint32_t* tab,
+                        uint32_t* out, uint32_t* partials, int blocks, hipStream_t st) {
+    hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, kPF, kNT>), dim3((unsigned)blocks), dim3(bkd::kBlock), 0, st,
+                       base, descs, count, tab, out, partials);
+}
+
+// Indexed batch through the chunked plan (plan_kernels.hpp). Scratch is stream-ordered.
+int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, const uint64_t* offsets,
+                const uint32_t* lengths, uint64_t n, const uint32_t* seeds, uint32_t seed_all, uint32_t* out,
+                hipStream_t st) {
+    if (n == 0) return BKD_OK;
+    if (n >= 0xFFFFFFF0ull) return fail(BKD_ERR_INVALID_ARG, "indexed batches hold fewer than 2^32 - 16 entries");
+    const int G = g_plan_lanes.load();
+    bkd::PlanGeo pg;
+    pg.step = 16u * (uint32_t)G;
+    pg.jc = (uint32_t)g_plan_jc.load();
+    pg.ch = pg.step * pg.jc;
+    pg.mis = (uint32_t)((uintptr_t)base & 15u);
+    pg.merge = (uint32_t)g_plan_merge.load();
+    pg.nbins = (pg.ch + pg.merge - 1u + pg.step - 1u) / pg.step + 1u;
+    const uint32_t* xtab = nullptr;
+    int rc = xtab_for(ds, algo, pg.ch, &xtab);
+    if (rc) return rc;
+    const uint64_t capacity = std::min<uint64_t>(n + size / pg.ch + 16, 0xFFFFFFF0ull);
+    const uint32_t nb = (uint32_t)((n + bkd::kPlanBlock - 1) / bkd::kPlanBlock);
+    const uint32_t ncols = pg.nbins + 1u;
+    uint32_t *blk = nullptr, *blkoff = nullptr, *hdr = nullptr, *run_start = nullptr, *pslot = nullptr,
+             *big = nullptr, *partials = nullptr;
+    bkd::PlanDesc* descs = nullptr;
+    hipError_t e = hipMallocAsync((void**)&blk, (size_t)nb * ncols * 4, st);
+    if (e == hipSuccess) e = hipMallocAsync((void**)&blkoff, (size_t)nb * ncols * 4, st);
+    if (e == hipSuccess) e = hipMallocAsync((void**)&hdr, bkd::kHdrWords * 4, st);
+    if (e == hipSuccess) e = hipMallocAsync((void**)&run_start, (size_t)n * 4, st);
+    if (e == hipSuccess) e = hipMallocAsync((void**)&pslot, (size_t)n * 4, st);
+    if (e == hipSuccess) e = hipMallocAsync((void**)&big, (size_t)n * 4, st);
+    if (e == hipSuccess) e = hipMallocAsync((void**)&partials, (size_t)capacity * 4, st);
+    if (e == hipSuccess) e = hipMallocAsync((void**)&descs, (size_t)capacity * sizeof(bkd::PlanDesc), st);
+    if (e != hipSuccess) {
+        rc = fail(BKD_ERR_NOMEM, std::string("plan scratch: ") + hipGetErrorString(e));
+    } else {
+        hipLaunchKernelGGL(bkd::plan_count_kernel, dim3(nb), dim3(bkd::kPlanBlock), 0, st, offsets, lengths, size, n,
+                           pg, blk);
+        hipLaunchKernelGGL(bkd::plan_scan_kernel, dim3(1), dim3(bkd::kPlanBlock), 0, st, blk, nb, pg, capacity,
+                           blkoff, hdr);
+        hipLaunchKernelGGL(bkd::plan_emit_kernel, dim3(nb), dim3(bkd::kPlanBlock), 0, st, offsets, lengths, seeds,
+                           seed_all, size, n, pg, capacity, blkoff, pslot, run_start, big, hdr, descs);
+        hipLaunchKernelGGL(bkd::plan_expand_big_kernel, dim3((unsigned)ds.cus), dim3(256), 0, st, offsets, lengths,
+                           seeds, seed_all, size, pg, pslot, run_start, big, hdr, descs);
+        const uint32_t* tab = ds.tables[algo][lane_index(G)];
+        switch (G) {
+            case 4: launch_plan_chunks<4>(base, descs, hdr + bkd::kHdrWork, tab, out, partials, ds.cus, st); break;
+            case 8: launch_plan_chunks<8>(base, descs, hdr + bkd::kHdrWork, tab, out, partials, ds.cus, st); break;
+            default: launch_plan_chunks<16>(base, descs, hdr + bkd::kHdrWork, tab, out, partials, ds.cus, st); break;
+        }
+        const uint32_t* btab = tab + bkd::gf2::byte_table_offset(G);
+        hipLaunchKernelGGL(bkd::plan_combine_kernel, dim3((unsigned)((n + 1023) / 1024)), dim3(1024), 0, st, base,
+                           offsets, lengths, seeds, seed_all, size, n, pg, xtab, btab, pslot, partials, out, ds.err);
+        e = hipGetLastError();
+        if (e != hipSuccess) rc = fail(BKD_ERR_HIP, std::string("plan kernels: ") + hipGetErrorString(e));
+    }
+    for (void* p : {(void*)blk, (void*)blkoff, (void*)hdr, (void*)run_start, (void*)pslot, (void*)big,
+                    (void*)partials, (void*)descs})
+        if (p) (void)hipFreeAsync(p, st);
+    return rc;
+}
+
+int indexed_batch(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, const uint64_t* offsets,
+                  const uint32_t* lengths, uint64_t n, const uint32_t* seeds, uint32_t seed_all, uint32_t* out,
+                  hipStream_t st) {
+    const int mode = g_plan_mode.load();
+    const bool direct = mode == 1 || (mode == 0 && size <= kDirectMaxBytes);
+    if (!direct) return launch_plan(ds, algo, base, size, offsets, lengths, n, seeds, seed_all, out, st);
+    bkd::IndexedSrc src{n, offsets, lengths, seeds, seed_all, size, out};
+    return dispatch_lanes(ds, auto_lanes(n ? size / n : 0), algo, base, src, n, st);
 }
 
 bool valid_algo(int algo) { return algo == BKD_CRC32C || algo == BKD_CRC32; }
@@ -188,6 +301,26 @@ int bkd_set_group_lanes(int lanes) {
     return BKD_OK;
 }
 
+int bkd_set_plan_mode(int mode) {
+    if (mode < 0 || mode > 2) return fail(BKD_ERR_INVALID_ARG, "plan mode must be 0 (auto), 1 (direct) or 2 (plan)");
+    g_plan_mode.store(mode);
+    return BKD_OK;
+}
+
+int bkd_set_plan_geometry(int lanes, int steps_per_chunk, int merge_bytes) {
+    if (lanes != 4 && lanes != 8 && lanes != 16) return fail(BKD_ERR_INVALID_ARG, "plan lanes must be 4, 8 or 16");
+    if (steps_per_chunk < 1) return fail(BKD_ERR_INVALID_ARG, "steps_per_chunk must be >= 1");
+    const uint32_t step = 16u * (uint32_t)lanes, ch = step * (uint32_t)steps_per_chunk;
+    if (ch > 32768u) return fail(BKD_ERR_INVALID_ARG, "chunk size must be <= 32 KiB");
+    if (merge_bytes < 16 || (uint32_t)merge_bytes > ch) return fail(BKD_ERR_INVALID_ARG, "merge must be in [16, chunk]");
+    const uint32_t nbins = (ch + (uint32_t)merge_bytes - 1u + step - 1u) / step + 1u;
+    if (nbins + 1u > (uint32_t)bkd::kMaxJC + 2u) return fail(BKD_ERR_INVALID_ARG, "too many step bins");
+    g_plan_lanes.store(lanes);
+    g_plan_jc.store(steps_per_chunk);
+    g_plan_merge.store(merge_bytes);
+    return BKD_OK;
+}
+
 int bkd_get_group_lanes(int algo, uint64_t mean_len) {
     (void)algo;
     return auto_lanes(mean_len);
@@ -201,9 +334,8 @@ int bkd_crc_batch_uniform(int algo, const void* d_base, uint64_t stride, uint32_
     DeviceState* ds = nullptr;
     int rc = ensure_current(&ds);
     if (rc) return rc;
-    bkd::UniformSrc src{stride, entry_len, d_seeds, seed_all};
-    return dispatch_lanes(*ds, auto_lanes(entry_len), algo, (const uint8_t*)d_base, src, n, d_out,
-                          (hipStream_t)stream);
+    bkd::UniformSrc src{n, stride, entry_len, d_seeds, seed_all, d_out};
+    return dispatch_lanes(*ds, auto_lanes(entry_len), algo, (const uint8_t*)d_base, src, n, (hipStream_t)stream);
 }
 
 int bkd_crc_batch(int algo, const void* d_base, uint64_t base_size, const uint64_t* d_offsets,
@@ -215,9 +347,8 @@ int bkd_crc_batch(int algo, const void* d_base, uint64_t base_size, const uint64
     DeviceState* ds = nullptr;
     int rc = ensure_current(&ds);
     if (rc) return rc;
-    const uint64_t mean = n ? base_size / n : 0;
-    bkd::IndexedSrc src{d_offsets, d_lengths, d_seeds, seed_all, base_size};
-    return dispatch_lanes(*ds, auto_lanes(mean), algo, (const uint8_t*)d_base, src, n, d_out, (hipStream_t)stream);
+    return indexed_batch(*ds, algo, (const uint8_t*)d_base, base_size, d_offsets, d_lengths, n, d_seeds, seed_all,
+                         d_out, (hipStream_t)stream);
 }
 
 int bkd_stream_sync(void* stream) {
@@ -274,9 +405,7 @@ int bkd_crc_batch_host(int algo, const void* h_base, uint64_t base_size, const u
         cleanup();
         return fail(BKD_ERR_HIP, std::string("host batch staging: ") + hipGetErrorString(e));
     }
-    const uint64_t mean = base_size / n;
-    bkd::IndexedSrc src{d_off, d_len, d_seeds, seed_all, base_size};
-    rc = dispatch_lanes(*ds, auto_lanes(mean), algo, d_base, src, n, d_out, st);
+    rc = indexed_batch(*ds, algo, d_base, base_size, d_off, d_len, n, d_seeds, seed_all, d_out, st);
     if (rc == BKD_OK) {
         e = hipMemcpyAsync(h_out, d_out, n * 4, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
@@ -311,8 +440,7 @@ int bkd_resume(int algo, uint32_t current, const void* ptr, uint64_t len, uint32
         BKD_HIP(hipMalloc(&d_out, 4));
         BKD_HIP(hipMemcpy(d_off, &off, 8, hipMemcpyHostToDevice));
         BKD_HIP(hipMemcpy(d_len, &l32, 4, hipMemcpyHostToDevice));
-        bkd::IndexedSrc src{d_off, d_len, nullptr, current, len};
-        rc = dispatch_lanes(*ds, auto_lanes(len), algo, (const uint8_t*)ptr, src, 1, d_out, nullptr);
+        rc = indexed_batch(*ds, algo, (const uint8_t*)ptr, len, d_off, d_len, 1, nullptr, current, d_out, nullptr);
         if (rc == BKD_OK) {
             hipError_t e = hipMemcpy(out, d_out, 4, hipMemcpyDeviceToHost);
             if (e != hipSuccess) rc = fail(BKD_ERR_HIP, hipGetErrorString(e));
@@ -341,13 +469,13 @@ int bkd_digest_package_batch(int algo, int64_t ledger_id, const int64_t* d_entry
     hipStream_t st = (hipStream_t)stream;
     const int lanes = auto_lanes(payload_size / n);
     const uint32_t* tab = ds->tables[algo][lane_index(lanes)];
-    const uint32_t* btab = tab + (bkd::gf2::compact_words(lanes) - 256);
+    const uint32_t* btab = tab + bkd::gf2::byte_table_offset(lanes);
     const unsigned blocks = (unsigned)((n + 255) / 256);
     hipLaunchKernelGGL(bkd::package_header_kernel, dim3(blocks), dim3(256), 0, st, btab, ledger_id, d_entry_ids,
                        d_lacs, d_length_fields, n, (uint8_t*)d_frames, frame_stride, d_digests);
     BKD_HIP(hipGetLastError());
-    bkd::IndexedSrc src{d_offsets, d_lengths, d_digests, 0u, payload_size};
-    rc = dispatch_lanes(*ds, lanes, algo, (const uint8_t*)d_payload, src, n, d_digests, st);
+    bkd::IndexedSrc src{n, d_offsets, d_lengths, d_digests, 0u, payload_size, d_digests};
+    rc = dispatch_lanes(*ds, lanes, algo, (const uint8_t*)d_payload, src, n, st);
     if (rc) return rc;
     hipLaunchKernelGGL(bkd::package_digest_kernel, dim3(blocks), dim3(256), 0, st, d_digests, n,
                        (uint8_t*)d_frames, frame_stride, mac);
@@ -373,14 +501,14 @@ int bkd_digest_verify_batch(int algo, int64_t ledger_id, int64_t first_entry_id,
     }
     const int lanes = auto_lanes(framed_size / n);
     const uint32_t* tab = ds->tables[algo][lane_index(lanes)];
-    const uint32_t* btab = tab + (bkd::gf2::compact_words(lanes) - 256);
+    const uint32_t* btab = tab + bkd::gf2::byte_table_offset(lanes);
     const unsigned blocks = (unsigned)((n + 255) / 256);
     uint32_t* scratch = reinterpret_cast<uint32_t*>(d_status);
     hipLaunchKernelGGL(bkd::verify_header_kernel, dim3(blocks), dim3(256), 0, st, btab, (const uint8_t*)d_framed,
                        framed_size, d_offsets, d_lengths, n, mac, scratch, d_first_bad);
     BKD_HIP(hipGetLastError());
-    bkd::FramedPayloadSrc src{d_offsets, d_lengths, scratch, framed_size, mac};
-    rc = dispatch_lanes(*ds, lanes, algo, (const uint8_t*)d_framed, src, n, scratch, st);
+    bkd::FramedPayloadSrc src{n, d_offsets, d_lengths, scratch, framed_size, mac};
+    rc = dispatch_lanes(*ds, lanes, algo, (const uint8_t*)d_framed, src, n, st);
     if (rc) return rc;
     hipLaunchKernelGGL(bkd::verify_finish_kernel, dim3(blocks), dim3(256), 0, st, (const uint8_t*)d_framed,
                        framed_size, d_offsets, d_lengths, n, mac, ledger_id, first_entry_id, skip_entry_check,

@@ -37,10 +37,14 @@ template <int G>
 struct Geo {
     static_assert(G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "group width");
     static constexpr int kLevels = G == 4 ? 2 : G == 8 ? 3 : G == 16 ? 4 : G == 32 ? 5 : 6;
-    static constexpr int kCompactWords = (2 + kLevels) * 1024 + 256;
-    static constexpr int kAuxWords = kCompactWords - 1024;  // everything but the main operator
-    static constexpr uint32_t kX32Off = kMainBytes;         // LDS byte offset of the x^32 set
+    // Groups of <= 16 lanes sit inside one DPP row and have LDS room for the x^64/x^96 sets.
+    static constexpr bool kFast = G <= 16;
+    static constexpr int kCompactWords = (2 + kLevels) * 1024 + 256 + 2048;
+    static constexpr int kAuxWords = kCompactWords - 1024 - (kFast ? 0 : 2048);  // staged after the main set
+    static constexpr uint32_t kX32Off = kMainBytes;  // LDS byte offset of the x^32 set
     static constexpr uint32_t kByteTabOff = kMainBytes + (1 + kLevels) * 4096u;
+    static constexpr uint32_t kX64Off = kByteTabOff + 1024u;
+    static constexpr uint32_t kX96Off = kX64Off + 4096u;
     static constexpr int kLdsWords = (int)(kMainBytes / 4) + kAuxWords;
     static constexpr int64_t kStep = 16 * G;
 };
@@ -98,67 +102,120 @@ __device__ __forceinline__ uint32_t place_seed(uint32_t r, int64_t d) {
     return 0u;
 }
 
-// ---- entry sources: where entry i lives, how long it is, what it resumes from ----
-// get() returns 0 = compute, 1 = skip (out = 0), 2 = out of bounds (out = 0, flag).
+// ---- work sources ---------------------------------------------------------------------
+// get(w, it) describes work item w: the byte range [s, s+len) of `base`, the raw register r0
+// folded into its first bytes (~seed for a whole entry or a chunk at an entry's head, 0 for an
+// inner chunk), and where the result goes: *dst = reg ^ xorout (~0 = finalized CRC, 0 = raw
+// partial register). Return: 0 compute, 1 write 0 to *dst, 2 out of bounds (write 0, flag),
+// 3 nothing to do.
+
+struct Work {
+    int64_t s;
+    uint32_t len;
+    uint32_t r0;
+    uint32_t* dst;
+    uint32_t xorout;
+};
 
 struct UniformSrc {
+    uint64_t n;
     uint64_t stride;
     uint32_t len;
     const uint32_t* seeds;
     uint32_t seed_all;
-    __device__ __forceinline__ int get(uint64_t i, int64_t& off, uint32_t& n, uint32_t& seed) const {
-        off = (int64_t)(i * stride);
-        n = len;
-        seed = seeds ? seeds[i] : seed_all;
+    uint32_t* out;
+    __device__ __forceinline__ uint64_t count() const { return n; }
+    __device__ __forceinline__ int get(uint64_t i, Work& w) const {
+        w.s = (int64_t)(i * stride);
+        w.len = len;
+        w.r0 = ~(seeds ? seeds[i] : seed_all);
+        w.dst = out + i;
+        w.xorout = 0xFFFFFFFFu;
         return 0;
     }
 };
 
 struct IndexedSrc {
+    uint64_t n;
     const uint64_t* offsets;
     const uint32_t* lengths;
     const uint32_t* seeds;
     uint32_t seed_all;
     uint64_t size;
-    __device__ __forceinline__ int get(uint64_t i, int64_t& off, uint32_t& n, uint32_t& seed) const {
+    uint32_t* out;
+    __device__ __forceinline__ uint64_t count() const { return n; }
+    __device__ __forceinline__ int get(uint64_t i, Work& w) const {
         const uint64_t o = offsets[i];
         const uint32_t l = lengths[i];
+        w.dst = out + i;
         if (o > size || (uint64_t)l > size - o) return 2;
-        off = (int64_t)o;
-        n = l;
-        seed = seeds ? seeds[i] : seed_all;
+        w.s = (int64_t)o;
+        w.len = l;
+        w.r0 = ~(seeds ? seeds[i] : seed_all);
+        w.xorout = 0xFFFFFFFFu;
         return 0;
     }
 };
 
 // Framed entry [32 B header][mac][payload]: CRC the payload resuming from the header CRC
-// already stored in seeds[i] (DigestManager.java:236-239).
+// already stored in seeds[i] (DigestManager.java:236-239); result over seeds[i] in place.
 struct FramedPayloadSrc {
+    uint64_t n;
     const uint64_t* offsets;
     const uint32_t* lengths;
-    const uint32_t* seeds;
+    uint32_t* seeds;
     uint64_t size;
     uint32_t mac;
-    __device__ __forceinline__ int get(uint64_t i, int64_t& off, uint32_t& n, uint32_t& seed) const {
+    __device__ __forceinline__ uint64_t count() const { return n; }
+    __device__ __forceinline__ int get(uint64_t i, Work& w) const {
         const uint64_t o = offsets[i];
         const uint32_t l = lengths[i];
+        w.dst = seeds + i;
         if (o > size || (uint64_t)l > size - o) return 2;
         if (l < 32u + mac) return 1;
-        off = (int64_t)(o + 32u + mac);
-        n = l - 32u - mac;
-        seed = seeds[i];
+        w.s = (int64_t)(o + 32u + mac);
+        w.len = l - 32u - mac;
+        w.r0 = ~seeds[i];
+        w.xorout = 0xFFFFFFFFu;
         return 0;
     }
 };
 
-template <int G, int PF, bool NT, class Src>
-__global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __restrict__ base, Src src, uint64_t n,
-                                                            const uint32_t* __restrict__ tables,
-                                                            uint32_t* __restrict__ out, uint32_t* __restrict__ err) {
-    using Gm = Geo<G>;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[Gm::kLdsWords];
+// DPP row_shl:SH — lane i receives lane i + SH of its 16-lane row (0 past the row end).
+template <int SH>
+__device__ __forceinline__ uint32_t dpp_row_shl(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x100 | SH, 0xF, 0xF, false);
+}
 
-    // Stage the operator tables: main operator replicated per bank, the rest compact.
+// Lane tree for groups inside one DPP row: at level LV lane g folds lane g + 2^LV's block,
+// v = v * x^(128*2^LV) ^ v[g + 2^LV]. Lane 0 of the group only ever combines lanes of its own
+// group (g + 2^LV < G on every path that reaches it), so the result is valid in lane 0.
+template <int LV, int LEVELS>
+__device__ __forceinline__ uint32_t lane_tree_dpp(const uint32_t* lds, uint32_t x32_off, uint32_t v) {
+    if constexpr (LV == LEVELS) {
+        return v;
+    } else {
+        const uint32_t other = dpp_row_shl<(1 << LV)>(v);
+        v = mul_aux(lds, x32_off + 4096u * (uint32_t)(1 + LV), v) ^ other;
+        return lane_tree_dpp<LV + 1, LEVELS>(lds, x32_off, v);
+    }
+}
+
+// Zero the low d bytes (1..15) of a 16-byte little-endian vector.
+__device__ __forceinline__ u32x4 mask_low_bytes(u32x4 w, uint32_t d) {
+    auto m = [](uint32_t x, int32_t k) -> uint32_t {  // k = bytes of this dword to clear
+        return k >= 4 ? 0u : (k <= 0 ? x : x & (0xFFFFFFFFu << (8 * k)));
+    };
+    w.x = m(w.x, (int32_t)d);
+    w.y = m(w.y, (int32_t)d - 4);
+    w.z = m(w.z, (int32_t)d - 8);
+    w.w = m(w.w, (int32_t)d - 12);
+    return w;
+}
+
+// Stage the operator tables: the main operator replicated per bank, the rest compact.
+template <int G>
+__device__ __forceinline__ void stage_tables(uint32_t* lds, const uint32_t* __restrict__ tables) {
     for (int idx = threadIdx.x; idx < 4 * 256 * 8; idx += kBlock) {
         const int q = idx & 7, b = (idx >> 3) & 255, t = idx >> 11;
         const uint32_t v = tables[t * 256 + b];
@@ -166,69 +223,49 @@ __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __res
                               (uint32_t)q * 16u;
         *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(lds) + addr) = u32x4{v, v, v, v};
     }
-    for (int idx = threadIdx.x; idx < Gm::kAuxWords; idx += kBlock) lds[kMainBytes / 4 + idx] = tables[1024 + idx];
+    for (int idx = threadIdx.x; idx < Geo<G>::kAuxWords; idx += kBlock) lds[kMainBytes / 4 + idx] = tables[1024 + idx];
     __syncthreads();
+}
 
-    const int lane = threadIdx.x & 63;
-    const int g = lane & (G - 1);
-    const uint32_t lanereg = ((uint32_t)(lane & 31) << 2) | (1u << 16);
-    const uint64_t ngroups = (uint64_t)gridDim.x * (kBlock / G);
-    const uint64_t gid = (uint64_t)blockIdx.x * (kBlock / G) + (uint64_t)(threadIdx.x / G);
+// Raw CRC register of base[s, e) (e - s >= 16 unless ALIGNED), with the register r0 folded into
+// its first 4 bytes, computed by the G lanes of one group; the result is valid in lane g == 0.
+// ALIGNED: `e` is 16-byte aligned in device memory, so every lane address is aligned; the lane
+// straddling s loads its aligned block and clears the bytes before s (any e - s >= 1 works).
+// Otherwise the straddling lane loads 16 bytes at s (needs e - s >= 16) and shifts them up.
+template <int G, int PF, bool NT, bool ALIGNED>
+__device__ __forceinline__ uint32_t fold_range(const uint32_t* lds, uint32_t lanereg, int g,
+                                               const uint8_t* __restrict__ base, int64_t s, int64_t e, uint32_t r0) {
+    using Gm = Geo<G>;
+    const uint32_t J = (uint32_t)((e - s + Gm::kStep - 1) / Gm::kStep);
+    const int64_t a = e - (int64_t)J * Gm::kStep + 16 * g;
 
-    for (uint64_t i = gid; i < n; i += ngroups) {
-        int64_t s;
-        uint32_t len, seed;
-        const int st = src.get(i, s, len, seed);
-        if (st != 0) {
-            if (g == 0) {
-                out[i] = 0u;
-                if (st == 2 && err) atomicOr(err, 1u);
-            }
-            continue;
-        }
-        if (len < 16u) {  // tiny entry: serial byte loop (ReflectedIntCrc.java:44-48 form)
-            if (g == 0) {
-                uint32_t r = ~seed;
-                const uint8_t* q = base + s;
-                for (uint32_t k = 0; k < len; ++k)
-                    r = lds_word(lds, Gm::kByteTabOff + (((r ^ q[k]) & 0xffu) << 2)) ^ (r >> 8);
-                out[i] = ~r;
-            }
-            continue;
-        }
+    // Step 0: masked head + seed fold.
+    u32x4 w;
+    if (a >= s) {
+        w = ld16<NT>(base + a);
+    } else if (a + 16 > s) {
+        if constexpr (ALIGNED) w = mask_low_bytes(ld16<NT>(base + a), (uint32_t)(s - a));
+        else w = shl_bytes(ld16<NT>(base + s), (uint32_t)(s - a));
+    } else {
+        w = u32x4{0u, 0u, 0u, 0u};
+    }
+    if (a < s + 4 && a + 16 > s) {
+        const int64_t d = s - a;
+        w.x ^= place_seed(r0, d);
+        w.y ^= place_seed(r0, d - 4);
+        w.z ^= place_seed(r0, d - 8);
+        w.w ^= place_seed(r0, d - 12);
+    }
+    // When the range starts in the last 3 bytes of step 0's window, the tail of the seed
+    // image spills into dword 0 of lane 0 at step 1; fx carries it into that first fold.
+    uint32_t fx = 0u;
+    if (a + Gm::kStep < s + 4) fx = place_seed(r0, s - (a + Gm::kStep));
+    uint32_t c0 = w.x, c1 = w.y, c2 = w.z, c3 = w.w;
 
-        const uint32_t J = (uint32_t)((len + Gm::kStep - 1) / Gm::kStep);
-        const int64_t e = s + (int64_t)len;
-        const int64_t a = e - (int64_t)J * Gm::kStep + 16 * g;
-
-        // Step 0: masked head + seed fold.
-        u32x4 w;
-        if (a >= s) {
-            w = ld16<NT>(base + a);
-        } else if (a + 16 > s) {
-            w = shl_bytes(ld16<NT>(base + s), (uint32_t)(s - a));
-        } else {
-            w = u32x4{0u, 0u, 0u, 0u};
-        }
-        const uint32_t r0 = ~seed;
-        if (a < s + 4 && a + 16 > s) {
-            const int64_t d = s - a;
-            w.x ^= place_seed(r0, d);
-            w.y ^= place_seed(r0, d - 4);
-            w.z ^= place_seed(r0, d - 8);
-            w.w ^= place_seed(r0, d - 12);
-        }
-        // When the entry starts in the last 3 bytes of step 0's window, the tail of the seed
-        // image spills into dword 0 of lane 0 at step 1; fx carries it into that first fold.
-        uint32_t fx = 0u;
-        if (a + Gm::kStep < s + 4) fx = place_seed(r0, s - (a + Gm::kStep));
-        uint32_t c0 = w.x, c1 = w.y, c2 = w.z, c3 = w.w;
-
-        // Steps 1..J-1 with PF loads in flight per lane. The steady-state loop issues its
-        // loads unconditionally (a conditional load would merge registers and force an
-        // early vmcnt(0)); only the < PF-step tail is handled with guarded code.
-        const uint8_t* p = base + a + Gm::kStep;
-        const uint32_t rem = J - 1u;
+    // Steps 1..J-1 with PF loads in flight per lane. The steady-state loop issues its loads
+    // unconditionally (a conditional load would merge registers and force an early vmcnt(0)).
+    const uint8_t* p = base + a + Gm::kStep;
+    const uint32_t rem = J - 1u;
 #define BKD_FOLD0(d)                                     \
     do {                                                 \
         c0 = mul_main(lds, c0, lanereg) ^ (d).x ^ fx;    \
@@ -244,53 +281,59 @@ __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __res
         c2 = mul_main(lds, c2, lanereg) ^ (d).z;     \
         c3 = mul_main(lds, c3, lanereg) ^ (d).w;     \
     } while (0)
-        if (rem >= (uint32_t)PF) {
-            // A/B register double buffer: fold one block while the other block's loads fly.
-            u32x4 A[PF], B[PF];
+    if (rem >= (uint32_t)PF) {
+        // A/B register double buffer: fold one block while the other block's loads fly.
+        u32x4 A[PF], B[PF];
 #pragma unroll
-            for (int k = 0; k < PF; ++k) A[k] = ld16<NT>(p + (int64_t)k * Gm::kStep);
-            p += (int64_t)PF * Gm::kStep;  // p = first step not yet loaded
-            uint32_t left = rem - (uint32_t)PF;
-            while (left >= 2u * PF) {
+        for (int k = 0; k < PF; ++k) A[k] = ld16<NT>(p + (int64_t)k * Gm::kStep);
+        p += (int64_t)PF * Gm::kStep;  // p = first step not yet loaded
+        uint32_t left = rem - (uint32_t)PF;
+        while (left >= 2u * PF) {
 #pragma unroll
-                for (int k = 0; k < PF; ++k) B[k] = ld16<NT>(p + (int64_t)k * Gm::kStep);
-                BKD_FOLD0(A[0]);
-#pragma unroll
-                for (int k = 1; k < PF; ++k) BKD_FOLD(A[k]);
-#pragma unroll
-                for (int k = 0; k < PF; ++k) A[k] = ld16<NT>(p + (int64_t)(PF + k) * Gm::kStep);
-#pragma unroll
-                for (int k = 0; k < PF; ++k) BKD_FOLD(B[k]);
-                p += (int64_t)(2 * PF) * Gm::kStep;
-                left -= 2u * PF;
-            }
-            // Tail: A holds PF loaded steps; `left` (< 2PF) steps remain unloaded.
-#pragma unroll
-            for (int k = 0; k < PF; ++k)
-                if ((uint32_t)k < left) B[k] = ld16<NT>(p + (int64_t)k * Gm::kStep);
+            for (int k = 0; k < PF; ++k) B[k] = ld16<NT>(p + (int64_t)k * Gm::kStep);
             BKD_FOLD0(A[0]);
 #pragma unroll
             for (int k = 1; k < PF; ++k) BKD_FOLD(A[k]);
 #pragma unroll
-            for (int k = 0; k < PF; ++k)
-                if ((uint32_t)(PF + k) < left) A[k] = ld16<NT>(p + (int64_t)(PF + k) * Gm::kStep);
+            for (int k = 0; k < PF; ++k) A[k] = ld16<NT>(p + (int64_t)(PF + k) * Gm::kStep);
 #pragma unroll
-            for (int k = 0; k < PF; ++k)
-                if ((uint32_t)k < left) BKD_FOLD(B[k]);
-#pragma unroll
-            for (int k = 0; k < PF; ++k)
-                if ((uint32_t)(PF + k) < left) BKD_FOLD(A[k]);
-        } else {
-            for (uint32_t k = 0; k < rem; ++k) {
-                const u32x4 d = ld16<NT>(p + (int64_t)k * Gm::kStep);
-                BKD_FOLD0(d);
-            }
+            for (int k = 0; k < PF; ++k) BKD_FOLD(B[k]);
+            p += (int64_t)(2 * PF) * Gm::kStep;
+            left -= 2u * PF;
         }
+        // Tail: A holds PF loaded steps; `left` (< 2PF) steps remain unloaded.
+#pragma unroll
+        for (int k = 0; k < PF; ++k)
+            if ((uint32_t)k < left) B[k] = ld16<NT>(p + (int64_t)k * Gm::kStep);
+        BKD_FOLD0(A[0]);
+#pragma unroll
+        for (int k = 1; k < PF; ++k) BKD_FOLD(A[k]);
+#pragma unroll
+        for (int k = 0; k < PF; ++k)
+            if ((uint32_t)(PF + k) < left) A[k] = ld16<NT>(p + (int64_t)(PF + k) * Gm::kStep);
+#pragma unroll
+        for (int k = 0; k < PF; ++k)
+            if ((uint32_t)k < left) BKD_FOLD(B[k]);
+#pragma unroll
+        for (int k = 0; k < PF; ++k)
+            if ((uint32_t)(PF + k) < left) BKD_FOLD(A[k]);
+    } else {
+        for (uint32_t k = 0; k < rem; ++k) {
+            const u32x4 d = ld16<NT>(p + (int64_t)k * Gm::kStep);
+            BKD_FOLD0(d);
+        }
+    }
 #undef BKD_FOLD
 #undef BKD_FOLD0
 
-        // Finish: lane Horner (x^32), lane tree (x^(128*2^s)), final x^32.
-        uint32_t v = mul_aux(lds, Gm::kX32Off, c0) ^ c1;
+    // Finish: in-lane combine of the 4 streams (x^96, x^64, x^32), lane tree (x^(128*2^s)),
+    // final x^32. Groups inside a DPP row shift with row_shl (VALU latency) instead of ds_bpermute.
+    uint32_t v;
+    if constexpr (Gm::kFast) {
+        v = mul_aux(lds, Gm::kX96Off, c0) ^ mul_aux(lds, Gm::kX64Off, c1) ^ mul_aux(lds, Gm::kX32Off, c2) ^ c3;
+        v = lane_tree_dpp<0, Gm::kLevels>(lds, Gm::kX32Off, v);
+    } else {
+        v = mul_aux(lds, Gm::kX32Off, c0) ^ c1;
         v = mul_aux(lds, Gm::kX32Off, v) ^ c2;
         v = mul_aux(lds, Gm::kX32Off, v) ^ c3;
 #pragma unroll
@@ -298,8 +341,97 @@ __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __res
             const uint32_t other = (uint32_t)__shfl_xor((int)v, 1 << lv);
             v = mul_aux(lds, Gm::kX32Off + 4096u * (uint32_t)(1 + lv), v) ^ other;
         }
-        v = mul_aux(lds, Gm::kX32Off, v);
-        if (g == 0) out[i] = ~v;
+    }
+    return mul_aux(lds, Gm::kX32Off, v);
+}
+
+// One CRC per work item of `src` (uniform / indexed / framed-payload entries), persistent grid.
+template <int G, int PF, bool NT, class Src>
+__global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __restrict__ base, Src src,
+                                                            const uint32_t* __restrict__ tables,
+                                                            uint32_t* __restrict__ err) {
+    using Gm = Geo<G>;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[Gm::kLdsWords];
+    stage_tables<G>(lds, tables);
+
+    const int lane = threadIdx.x & 63;
+    const int g = lane & (G - 1);
+    const uint32_t lanereg = ((uint32_t)(lane & 31) << 2) | (1u << 16);
+    const uint64_t ngroups = (uint64_t)gridDim.x * (kBlock / G);
+    const uint64_t gid = (uint64_t)blockIdx.x * (kBlock / G) + (uint64_t)(threadIdx.x / G);
+
+    const uint64_t n = src.count();
+    for (uint64_t i = gid; i < n; i += ngroups) {
+        Work wk;
+        const int st = src.get(i, wk);
+        if (st != 0) {
+            if (g == 0 && st != 3) {
+                *wk.dst = 0u;
+                if (st == 2 && err) atomicOr(err, 1u);
+            }
+            continue;
+        }
+        if (wk.len < 16u) {  // tiny range: serial byte loop (ReflectedIntCrc.java:44-48 form)
+            if (g == 0) {
+                uint32_t r = wk.r0;
+                const uint8_t* q = base + wk.s;
+                for (uint32_t k = 0; k < wk.len; ++k)
+                    r = lds_word(lds, Gm::kByteTabOff + (((r ^ q[k]) & 0xffu) << 2)) ^ (r >> 8);
+                *wk.dst = r ^ wk.xorout;
+            }
+            continue;
+        }
+        const uint32_t v =
+            fold_range<G, PF, NT, false>(lds, lanereg, g, base, wk.s, wk.s + (int64_t)wk.len, wk.r0);
+        if (g == 0) *wk.dst = v ^ wk.xorout;
+    }
+}
+
+// ---- chunk descriptors of the ragged-batch plan (built by plan_kernels.hpp) ----
+// 16 bytes: s (48-bit byte offset) | len (16 bits; a chunk is at most CH + 15 < 64 KiB bytes),
+// the register folded into its first bytes, and the destination (bit 31: finalized CRC into
+// out[dst], else raw partial into partials[dst]). len == 0 marks a hole (skipped).
+constexpr uint32_t kPlanFinal = 0x80000000u;
+
+struct __attribute__((aligned(16))) PlanDesc {
+    uint64_t s_len;
+    uint32_t r0;
+    uint32_t dst;
+};
+
+// One chunk per group, descriptors read one round ahead (prefetch) so the next chunk's
+// geometry is in registers when the current chunk finishes.
+template <int G, int PF, bool NT>
+__global__ void __launch_bounds__(kBlock) crc_plan_chunks_kernel(const uint8_t* __restrict__ base,
+                                                                 const PlanDesc* __restrict__ descs,
+                                                                 const uint32_t* __restrict__ count,
+                                                                 const uint32_t* __restrict__ tables,
+                                                                 uint32_t* __restrict__ out,
+                                                                 uint32_t* __restrict__ partials) {
+    using Gm = Geo<G>;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[Gm::kLdsWords];
+    stage_tables<G>(lds, tables);
+
+    const int lane = threadIdx.x & 63;
+    const int g = lane & (G - 1);
+    const uint32_t lanereg = ((uint32_t)(lane & 31) << 2) | (1u << 16);
+    const uint64_t ngroups = (uint64_t)gridDim.x * (kBlock / G);
+    const uint64_t gid = (uint64_t)blockIdx.x * (kBlock / G) + (uint64_t)(threadIdx.x / G);
+    const uint64_t n = *count;
+    if (gid >= n) return;
+    PlanDesc nx = descs[gid];
+    for (uint64_t i = gid; i < n; i += ngroups) {
+        const PlanDesc d = nx;
+        const uint64_t ni = i + ngroups < n ? i + ngroups : i;  // unconditional, clamped prefetch
+        nx = descs[ni];
+        const int64_t s = (int64_t)(d.s_len & 0xFFFFFFFFFFFFull);
+        const int64_t len = (int64_t)(d.s_len >> 48);
+        if (len == 0) continue;
+        const uint32_t v = fold_range<G, PF, NT, true>(lds, lanereg, g, base, s, s + len, d.r0);
+        if (g == 0) {
+            if (d.dst & kPlanFinal) out[d.dst & ~kPlanFinal] = ~v;
+            else partials[d.dst] = v;
+        }
     }
 }
 

@@ -59,17 +59,21 @@ inline int log2_lanes(int lanes) {
 //   set 0                : C_main = x^(128*lanes)   (one step of every lane stream, stride 16*lanes bytes)
 //   set 1                : x^32                     (dword-to-dword inside a lane)
 //   set 2+s, s<log2 lanes: x^(128 * 2^s)            (lane-tree level s: a block of 2^s lanes = 16*2^s bytes)
-//   trailing 256 words   : byte table x^8           (serial path for tiny entries; equals ReflectedIntCrc's table)
-inline int64_t compact_words(int lanes) { return (int64_t)(2 + log2_lanes(lanes)) * 1024 + 256; }
+//   256 words            : byte table x^8           (serial paths; equals ReflectedIntCrc's table)
+//   2 more sets          : x^64, x^96               (one-level in-lane combine of the 4 dword streams)
+inline int64_t byte_table_offset(int lanes) { return (int64_t)(2 + log2_lanes(lanes)) * 1024; }
+inline int64_t compact_words(int lanes) { return byte_table_offset(lanes) + 256 + 2048; }
 
 inline int64_t build_compact(int algo, int lanes, uint32_t* out) {
     const int levels = log2_lanes(lanes);
     operator_tables(algo, xpow(algo, 128ull * (uint64_t)lanes), out);
     operator_tables(algo, xpow(algo, 32), out + 1024);
     for (int s = 0; s < levels; ++s) operator_tables(algo, xpow(algo, 128ull << s), out + 2048 + 1024 * s);
-    uint32_t* bt = out + (2 + levels) * 1024;
+    uint32_t* bt = out + byte_table_offset(lanes);
     const uint32_t x8 = xpow(algo, 8);
     for (uint32_t b = 0; b < 256; ++b) bt[b] = mul(algo, b, x8);
+    operator_tables(algo, xpow(algo, 64), bt + 256);
+    operator_tables(algo, xpow(algo, 96), bt + 256 + 1024);
     return compact_words(lanes);
 }
 

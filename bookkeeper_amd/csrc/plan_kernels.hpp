@@ -1,0 +1,326 @@
+// Work plan for ragged (indexed) batches: aligned chunking, bucketing by step count, combine.
+//
+// Why: a G-lane group walks its work in lockstep with the other groups of its wavefront, so a
+// wave holding Zipf-sized entries runs as long as its longest entry (SURVEY.md §7 "load balance
+// for Zipf sizes"), and packed entries start and end at arbitrary bytes. The plan therefore
+//  * splits every entry [s, e) at ae = the last 16-byte-aligned device address <= e: the <= 15
+//    tail bytes [ae, e) are folded serially by plan_combine_kernel, everything before ae is cut
+//    into chunks of CH = 16*G*JC bytes whose ends are aligned (c = 0 ends at ae, c = m-1 is the
+//    head and starts at s, carrying the seed), so every 16-byte load of the main kernel is an
+//    aligned global_load_dwordx4;
+//  * lists the chunks in descending step count (merged heads JC+1, full chunks JC, heads JC-1..1)
+//    so that neighbouring groups, which run in lockstep, have equal work;
+//  * writes one self-contained 32-byte descriptor per chunk (range, seed register, destination),
+//    which the main kernel prefetches one round ahead — no dependent index loads at chunk start;
+//  * combines multi-chunk entries as reg = sum_c partial_c * X^c, X = x^(8*CH) (Horner from the
+//    head), then folds the tail bytes: the GPU analogue of crc32c_chunk's stream merge by shift
+//    tables (crc32c_sse42.cpp:92-134).
+// Entries whose aligned part is < 16 bytes, invalid (out-of-bounds) entries, and entries that do
+// not fit the plan's capacity (only possible when entries overlap heavily) are computed serially by
+// plan_combine_kernel (correct, slow path).
+//
+// Launch sequence (caller's stream, no host sync): plan_count -> plan_scan -> plan_emit ->
+// plan_expand_big -> crc_plan_chunks_kernel -> plan_combine.
+#pragma once
+#include "crc_kernels.hpp"
+
+namespace bkd {
+
+constexpr int kPlanBlock = 1024;
+constexpr int kMaxJC = 128;  // bins 0 .. jc + merge steps
+constexpr uint32_t kEmitMax = 64;  // an emit thread writes at most this many full-chunk descriptors
+
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;  // single aligned chunk, no tail: the chunk writes out[] itself
+constexpr uint32_t kSerial = 0xFFFFFFFEu;  // whole entry folded serially by the combine kernel
+constexpr uint32_t kDirect = 0xFFFFFFFDu;  // plan capacity exceeded: serial too
+
+struct PlanGeo {
+    uint32_t step;   // 16 * G bytes
+    uint32_t jc;     // steps per full chunk
+    uint32_t ch;     // step * jc
+    uint32_t mis;    // device address of base modulo 16
+    uint32_t merge;  // a head chunk shorter than this (>= 16) merges into its neighbour
+    uint32_t nbins;  // bins 0 .. nbins-1: ceil((ch + merge - 1) / step) + 1
+};
+
+// hdr words
+constexpr int kHdrTotal = 0;  // all chunks
+constexpr int kHdrSlots = 1;  // partial slots
+constexpr int kHdrWork = 2;   // descriptors to process = min(total, capacity)
+constexpr int kHdrBig = 3;    // entries whose full chunks plan_expand_big writes
+constexpr int kHdrWords = 4;
+
+__device__ __forceinline__ bool entry_valid(uint64_t o, uint32_t l, uint64_t size) {
+    return !(o > size || (uint64_t)l > size - o);
+}
+
+struct EntryPlan {
+    int64_t s, e, ae;
+    uint32_t m;     // chunks of the aligned part
+    uint32_t jh;    // head chunk steps (1 .. nbins-1)
+    uint32_t full;  // chunks in the full bucket (bin JC)
+    uint32_t ps;    // partial slots (0: the single chunk writes the final CRC)
+    uint32_t kind;  // 0 chunked, 1 serial, 2 invalid
+};
+
+__device__ __forceinline__ EntryPlan plan_entry(uint64_t o, uint32_t l, uint64_t size, const PlanGeo& pg) {
+    EntryPlan p{};
+    if (!entry_valid(o, l, size)) {
+        p.kind = 2;
+        return p;
+    }
+    p.s = (int64_t)o;
+    p.e = (int64_t)(o + l);
+    const uint32_t delta = (uint32_t)((pg.mis + (uint64_t)p.e) & 15u);
+    p.ae = p.e - delta;
+    if (p.ae - p.s < 16) {
+        p.kind = 1;
+        return p;
+    }
+    const uint64_t la = (uint64_t)(p.ae - p.s);
+    uint32_t m = (uint32_t)((la + pg.ch - 1) / pg.ch);
+    uint64_t hl = la - (uint64_t)(m - 1u) * pg.ch;
+    if (hl < pg.merge && m > 1u) {  // a short head merges into its neighbour (up to ch + merge - 1 bytes)
+        --m;
+        hl += pg.ch;
+    }
+    p.m = m;
+    p.jh = (uint32_t)((hl + pg.step - 1) / pg.step);
+    p.full = (m - 1u) + (p.jh == pg.jc ? 1u : 0u);
+    p.ps = (m == 1u && delta == 0u) ? 0u : m;
+    p.kind = 0;
+    return p;
+}
+
+__device__ __forceinline__ PlanDesc chunk_desc(const EntryPlan& p, uint32_t c, uint32_t seed, uint32_t entry,
+                                               uint32_t slot, const PlanGeo& pg) {
+    PlanDesc d;
+    const int64_t e = p.ae - (int64_t)c * pg.ch;
+    const bool head = c + 1u == p.m;
+    const int64_t s = head ? p.s : e - (int64_t)pg.ch;
+    d.s_len = (uint64_t)s | ((uint64_t)(e - s) << 48);
+    d.r0 = head ? ~seed : 0u;
+    d.dst = p.ps == 0u ? (entry | kPlanFinal) : slot + c;
+    return d;
+}
+
+__device__ __forceinline__ PlanDesc skip_desc() { return PlanDesc{0ull, 0u, 0u}; }
+
+// Deterministic block-wide exclusive scan (1024 threads = 16 waves).
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t& total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, d);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int k = 0; k < kPlanBlock / 64; ++k) {
+            const uint32_t t = wsum[k];
+            wsum[k] = acc;
+            acc += t;
+        }
+        wsum[kPlanBlock / 64] = acc;
+    }
+    __syncthreads();
+    const uint32_t r = wsum[wave] + x - v;
+    total = wsum[kPlanBlock / 64];
+    __syncthreads();
+    return r;
+}
+
+// columns: bins 0 .. nbins-1 (chunk counts by step count; bin JC = full bucket), then slots.
+__device__ __forceinline__ uint32_t plan_ncols(const PlanGeo& pg) { return pg.nbins + 1u; }
+__device__ __forceinline__ uint32_t slot_col(const PlanGeo& pg) { return pg.nbins; }
+
+__global__ void __launch_bounds__(kPlanBlock) plan_count_kernel(const uint64_t* __restrict__ offsets,
+                                                                const uint32_t* __restrict__ lengths, uint64_t size,
+                                                                uint64_t n, PlanGeo pg, uint32_t* __restrict__ blk) {
+    __shared__ uint32_t col[kMaxJC + 2];
+    const uint32_t ncols = plan_ncols(pg);
+    for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) col[k] = 0u;
+    __syncthreads();
+    const uint64_t i = (uint64_t)blockIdx.x * kPlanBlock + threadIdx.x;
+    if (i < n) {
+        const EntryPlan p = plan_entry(offsets[i], lengths[i], size, pg);
+        if (p.kind == 0) {
+            if (p.jh != pg.jc) atomicAdd(&col[p.jh], 1u);
+            if (p.full) atomicAdd(&col[pg.jc], p.full);
+            if (p.ps) atomicAdd(&col[slot_col(pg)], p.ps);
+        }
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) blk[(uint64_t)k * gridDim.x + blockIdx.x] = col[k];
+}
+
+// One block: each wave scans whole columns across blocks (column-major, coalesced; 64 rows per
+// pass, carry in a register), then bins are placed in descending step count.
+__global__ void __launch_bounds__(kPlanBlock) plan_scan_kernel(const uint32_t* __restrict__ blk, uint32_t nb, PlanGeo pg,
+                                                               uint64_t capacity, uint32_t* __restrict__ blkoff,
+                                                               uint32_t* __restrict__ hdr) {
+    __shared__ uint32_t tot[kMaxJC + 2];
+    __shared__ uint32_t base[kMaxJC + 2];
+    const uint32_t ncols = plan_ncols(pg);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint32_t c = (uint32_t)wave; c < ncols; c += kPlanBlock / 64) {
+        const uint32_t* col = blk + (uint64_t)c * nb;
+        uint32_t* dst = blkoff + (uint64_t)c * nb;
+        uint32_t carry = 0;
+        for (uint32_t b1 = 0; b1 < nb; b1 += 64 * 16) {
+            uint32_t v[16];  // 16 rows per lane in flight before the dependent scans
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const uint32_t b = b1 + (uint32_t)r * 64 + (uint32_t)lane;
+                v[r] = b < nb ? col[b] : 0u;
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const uint32_t b = b1 + (uint32_t)r * 64 + (uint32_t)lane;
+                uint32_t x = v[r];
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t y = (uint32_t)__shfl_up((int)x, d);
+                    if (lane >= d) x += y;
+                }
+                if (b < nb) dst[b] = carry + x - v[r];
+                carry += (uint32_t)__shfl((int)x, 63);
+            }
+        }
+        if (lane == 0) tot[c] = carry;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int j = (int)pg.nbins - 1; j >= 0; --j) {  // descending step count (bin JC = full chunks)
+            base[j] = acc;
+            acc += tot[j];
+        }
+        base[slot_col(pg)] = 0;
+        hdr[kHdrTotal] = acc;
+        hdr[kHdrSlots] = tot[slot_col(pg)];
+        hdr[kHdrWork] = (uint32_t)((uint64_t)acc < capacity ? acc : capacity);
+        hdr[kHdrBig] = 0;
+    }
+    __syncthreads();
+    for (uint64_t k = threadIdx.x; k < (uint64_t)nb * ncols; k += kPlanBlock) blkoff[k] += base[k / nb];
+}
+
+__global__ void __launch_bounds__(kPlanBlock) plan_emit_kernel(const uint64_t* __restrict__ offsets,
+                                                               const uint32_t* __restrict__ lengths,
+                                                               const uint32_t* __restrict__ seeds, uint32_t seed_all,
+                                                               uint64_t size, uint64_t n, PlanGeo pg,
+                                                               uint64_t capacity, const uint32_t* __restrict__ blkoff,
+                                                               uint32_t* __restrict__ pslot,
+                                                               uint32_t* __restrict__ run_start,
+                                                               uint32_t* __restrict__ big, uint32_t* __restrict__ hdr,
+                                                               PlanDesc* __restrict__ descs) {
+    __shared__ uint32_t wsum[kPlanBlock / 64 + 1];
+    __shared__ uint32_t cursor[kMaxJC + 2];
+    const uint32_t ncols = plan_ncols(pg);
+    for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) cursor[k] = blkoff[(uint64_t)k * gridDim.x + blockIdx.x];
+    __syncthreads();
+    const uint64_t i = (uint64_t)blockIdx.x * kPlanBlock + threadIdx.x;
+    EntryPlan p{};
+    p.kind = 1;
+    if (i < n) p = plan_entry(offsets[i], lengths[i], size, pg);
+    const bool chunked = i < n && p.kind == 0;
+    uint32_t t_full, t_ps;
+    const uint32_t ex_full = block_excl_scan(chunked ? p.full : 0u, wsum, t_full);
+    const uint32_t ex_ps = block_excl_scan(chunked ? p.ps : 0u, wsum, t_ps);
+    if (i >= n) return;
+    if (!chunked) {
+        pslot[i] = kSerial;
+        return;
+    }
+    const uint32_t rs = cursor[pg.jc] + ex_full;
+    const uint32_t sb = cursor[slot_col(pg)] + ex_ps;
+    const bool has_head = p.jh != pg.jc;
+    const uint32_t hpos = has_head ? atomicAdd(&cursor[p.jh], 1u) : 0u;
+    const bool overflow = ((uint64_t)rs + p.full > capacity) || (has_head && (uint64_t)hpos >= capacity) ||
+                          (p.ps && (uint64_t)sb + p.ps > capacity);
+    run_start[i] = rs;
+    if (overflow) {
+        pslot[i] = kDirect;
+        for (uint32_t c = 0; c < p.full && (uint64_t)rs + c < capacity; ++c) descs[rs + c] = skip_desc();
+        if (has_head && (uint64_t)hpos < capacity) descs[hpos] = skip_desc();
+        return;
+    }
+    pslot[i] = p.ps ? sb : kNoSlot;
+    const uint32_t seed = seeds ? seeds[i] : seed_all;
+    if (has_head) descs[hpos] = chunk_desc(p, p.m - 1u, seed, (uint32_t)i, sb, pg);
+    if (p.full <= kEmitMax) {
+        for (uint32_t c = 0; c < p.full; ++c) descs[rs + c] = chunk_desc(p, c, seed, (uint32_t)i, sb, pg);
+    } else {
+        big[atomicAdd(&hdr[kHdrBig], 1u)] = (uint32_t)i;
+    }
+}
+
+// Full-bucket descriptors of entries with more than kEmitMax chunks: one block per entry.
+__global__ void plan_expand_big_kernel(const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ lengths,
+                                       const uint32_t* __restrict__ seeds, uint32_t seed_all, uint64_t size, PlanGeo pg,
+                                       const uint32_t* __restrict__ pslot, const uint32_t* __restrict__ run_start,
+                                       const uint32_t* __restrict__ big, const uint32_t* __restrict__ hdr,
+                                       PlanDesc* __restrict__ descs) {
+    const uint32_t nbig = hdr[kHdrBig];
+    for (uint32_t k = blockIdx.x; k < nbig; k += gridDim.x) {
+        const uint32_t i = big[k];
+        const EntryPlan p = plan_entry(offsets[i], lengths[i], size, pg);
+        const uint32_t seed = seeds ? seeds[i] : seed_all;
+        const uint32_t rs = run_start[i], sb = pslot[i];
+        for (uint32_t c = threadIdx.x; c < p.full; c += blockDim.x)
+            descs[rs + c] = chunk_desc(p, c, seed, i, sb, pg);
+    }
+}
+
+// Horner over the partial registers of each chunked entry, then its unaligned tail bytes;
+// serial fold of entries the plan did not chunk.
+__global__ void plan_combine_kernel(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets,
+                                    const uint32_t* __restrict__ lengths, const uint32_t* __restrict__ seeds,
+                                    uint32_t seed_all, uint64_t size, uint64_t n, PlanGeo pg,
+                                    const uint32_t* __restrict__ xtab, const uint32_t* __restrict__ btab,
+                                    const uint32_t* __restrict__ pslot, const uint32_t* __restrict__ partials,
+                                    uint32_t* __restrict__ out, uint32_t* __restrict__ err) {
+    __shared__ uint32_t X[1024];
+    __shared__ uint32_t B[256];
+    for (int k = threadIdx.x; k < 1024; k += blockDim.x) X[k] = xtab[k];
+    for (int k = threadIdx.x; k < 256; k += blockDim.x) B[k] = btab[k];
+    __syncthreads();
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t slot = pslot[i];
+    if (slot == kNoSlot) return;
+    const uint64_t o = offsets[i];
+    const uint32_t l = lengths[i];
+    if (!entry_valid(o, l, size)) {
+        out[i] = 0u;
+        if (err) atomicOr(err, 1u);
+        return;
+    }
+    if (slot == kSerial || slot == kDirect) {
+        uint32_t reg = ~(seeds ? seeds[i] : seed_all);
+        const uint8_t* q = base + o;
+        for (uint32_t k = 0; k < l; ++k) reg = B[(reg ^ q[k]) & 0xffu] ^ (reg >> 8);
+        out[i] = ~reg;
+        return;
+    }
+    const EntryPlan p = plan_entry(o, l, size, pg);
+    const uint32_t nq = (uint32_t)(p.e - p.ae);
+    // the tail [ae, e) lies in the aligned 16-byte block at ae: one vector load, no over-read past it
+    const u32x4 tail = nq ? *reinterpret_cast<const u32x4*>(base + p.ae) : u32x4{0u, 0u, 0u, 0u};
+    uint32_t reg = partials[slot + p.m - 1u];
+    for (int c = (int)p.m - 2; c >= 0; --c) {
+        reg = X[reg & 0xffu] ^ X[256 + ((reg >> 8) & 0xffu)] ^ X[512 + ((reg >> 16) & 0xffu)] ^ X[768 + (reg >> 24)];
+        reg ^= partials[slot + (uint32_t)c];
+    }
+    for (uint32_t k = 0; k < nq; ++k) {
+        const uint32_t w = k < 4 ? tail.x : k < 8 ? tail.y : k < 12 ? tail.z : tail.w;
+        reg = B[(reg ^ (w >> (8 * (k & 3)))) & 0xffu] ^ (reg >> 8);
+    }
+    out[i] = ~reg;
+}
+
+}  // namespace bkd

@@ -149,6 +149,13 @@ uint32_t bkd_host_xpow8n(int algo, uint64_t nbytes);
 
 /* Tuning: lanes per entry group (0 = automatic, else 4/8/16/32/64); prefetch is fixed at build. */
 int bkd_set_group_lanes(int lanes);
+/* Indexed-batch strategy: 0 = automatic (chunked plan unless the base buffer is <= 256 KiB),
+ * 1 = one entry per lane group, 2 = always the chunked plan. */
+int bkd_set_plan_mode(int mode);
+/* Chunked-plan geometry: lanes per group (4, 8 or 16), steps per full chunk (chunk = 16 * lanes *
+ * steps bytes, <= 32 KiB) and the head-merge threshold in bytes (a head chunk shorter than this
+ * joins its neighbour; >= 16). Default 8, 32, 16. */
+int bkd_set_plan_geometry(int lanes, int steps_per_chunk, int merge_bytes);
 int bkd_get_group_lanes(int algo, uint64_t mean_len);
 
 #ifdef __cplusplus

@@ -15,7 +15,9 @@ class KernelModel:
         self.main = t[0:1024]
         self.x32 = t[1024:2048]
         self.lv = [t[2048 + 1024 * s: 3072 + 1024 * s] for s in range(self.levels)]
-        self.byte = t[(2 + self.levels) * 1024:]
+        self.byte = t[(2 + self.levels) * 1024:(2 + self.levels) * 1024 + 256]
+        self.x64 = t[(2 + self.levels) * 1024 + 256:(2 + self.levels) * 1024 + 1280]
+        self.x96 = t[(2 + self.levels) * 1024 + 1280:(2 + self.levels) * 1024 + 2304]
 
     @staticmethod
     def _mul(tab, v: int) -> int:
@@ -69,9 +71,8 @@ class KernelModel:
             acc = [int(words[0, g, k]) for k in range(4)]
             for j in range(1, J):
                 acc = [self._mul(self.main, acc[k]) ^ int(words[j, g, k]) for k in range(4)]
-            v = self._mul(self.x32, acc[0]) ^ acc[1]
-            v = self._mul(self.x32, v) ^ acc[2]
-            v = self._mul(self.x32, v) ^ acc[3]
+            v = (self._mul(self.x96, acc[0]) ^ self._mul(self.x64, acc[1]) ^ self._mul(self.x32, acc[2])
+                 ^ acc[3])
             lane_vals.append(v)
         for s in range(self.levels):
             span = 1 << s
@@ -80,3 +81,42 @@ class KernelModel:
             assert len(lane_vals) == G >> (s + 1) and span
         total = self._mul(self.x32, lane_vals[0])
         return (~total) & 0xFFFFFFFF
+
+
+def plan_model(tables_by_lanes, algo_xpow8n, gf_mul, data: bytes, seed: int, lanes: int = 8, jc: int = 32,
+               mis: int = 0) -> int:
+    """Models the ragged-batch plan (plan_kernels.hpp) for one entry starting at a device address
+    congruent to `mis` (mod 16): the aligned part [0, ae) is cut into chunks of CH = 16*lanes*jc bytes
+    ending at aligned addresses (head chunk carries the seed; a head < 16 B merges into its
+    neighbour), each chunk folded by the kernel decomposition (aligned straddle masking), partial
+    registers combined by Horner with X = x^(8*CH), then the tail bytes [ae, e) folded serially."""
+    ch, step = 16 * lanes * jc, 16 * lanes
+    km = KernelModel(tables_by_lanes, lanes)
+    n = len(data)
+    byte = km.byte
+
+    def serial(reg, bs):
+        for b in bs:
+            reg = int(byte[(reg ^ b) & 0xFF]) ^ (reg >> 8)
+        return reg
+
+    ae = n - ((mis + n) & 15)
+    if ae < 16:
+        return (~serial((~seed) & 0xFFFFFFFF, data)) & 0xFFFFFFFF
+    m = (ae + ch - 1) // ch
+    hl = ae - (m - 1) * ch
+    if hl < 16 and m > 1:
+        m -= 1
+    parts = []
+    for c in range(m):
+        e = ae - c * ch
+        cs = 0 if c == m - 1 else e - ch
+        r0 = (~seed) & 0xFFFFFFFF if c == m - 1 else 0
+        # raw register of data[cs:e] with r0 folded in == ~KernelModel.crc(chunk, ~r0)
+        parts.append((~km.crc(data[cs:e], (~r0) & 0xFFFFFFFF)) & 0xFFFFFFFF)
+        assert (e - cs) <= ch + 15 and (e - cs + step - 1) // step <= jc + 1
+    X = algo_xpow8n(ch)
+    reg = parts[m - 1]
+    for c in range(m - 2, -1, -1):
+        reg = gf_mul(reg, X) ^ parts[c]
+    return (~serial(reg, data[ae:])) & 0xFFFFFFFF

@@ -23,8 +23,10 @@ LANES = (4, 8, 16, 32, 64)
 @pytest.fixture(autouse=True)
 def _auto_lanes():
     ck.set_group_lanes(0)
+    ck.set_plan_mode(0)
     yield
     ck.set_group_lanes(0)
+    ck.set_plan_mode(0)
 
 
 def _dev_bytes(torch, data: np.ndarray, dev):
@@ -123,11 +125,13 @@ def test_uniform_batches(gpu, algo, lanes):
 
 
 @pytest.mark.parametrize("algo", [ck.CRC32C, ck.CRC32])
-@pytest.mark.parametrize("lanes", LANES)
-def test_indexed_ragged_unaligned(gpu, algo, lanes):
-    """Random lengths 0..70000, random (unaligned, overlapping) offsets, random per-entry seeds."""
+@pytest.mark.parametrize("lanes,mode", [(l, 1) for l in LANES] + [(0, 2), (0, 0)])
+def test_indexed_ragged_unaligned(gpu, algo, lanes, mode):
+    """Random lengths 0..70000, random (unaligned, overlapping) offsets, random per-entry seeds;
+    mode 1 = one entry per lane group, mode 2 = chunked plan, mode 0 = automatic."""
     import torch
     ck.set_group_lanes(lanes)
+    ck.set_plan_mode(mode)
     rng = np.random.default_rng(lanes * 7 + algo)
     size = 3_000_000
     data = oracle.fill_splitmix64(size, 99)
@@ -283,3 +287,62 @@ def test_digest_batch_package_and_verify(gpu, dtype, algo):
                      for i in range(n)])
     assert (status == want).all()
     assert status[1234] != 0 and int(first_bad.item()) == 1234
+
+
+def test_plan_overflow_falls_back_to_direct(gpu):
+    """Heavily overlapping entries exceed the plan's capacity (n + size/CH + 16 chunks); the
+    overflowing entries are computed by the combine kernel's serial fallback, still bit-exact."""
+    import torch
+    ck.set_plan_mode(2)
+    size = 1 << 20
+    data = oracle.fill_splitmix64(size, 8)
+    n = 24
+    offs = np.zeros(n, dtype=np.int64)
+    offs[1::2] = 3
+    lens = np.full(n, size, dtype=np.int64)
+    lens[1::2] = size - 3
+    lens[5] = 100
+    base = _dev_bytes(torch, data, gpu)
+    got = ck.crc_batch(ck.CRC32C, base, torch.from_numpy(offs).to(gpu),
+                       torch.from_numpy(lens.astype(np.int32)).to(gpu), seed_all=0x1234, sync_check=True)
+    assert (got.cpu().numpy().view(np.uint32) == oracle.batch(0, data, offs, lens, seed_all=0x1234)).all()
+
+
+def test_plan_huge_single_entry_and_small_neighbours(gpu):
+    """A 96 MiB entry next to tiny ones: the plan spreads the big entry over the whole chip."""
+    import torch
+    size = 96 << 20
+    base = torch.empty(size + 1000, dtype=torch.uint8, device=gpu)
+    ck.fill_splitmix64(base, 77)
+    host = base.cpu().numpy()
+    offs = np.array([0, size, size + 10, size + 500, 7], dtype=np.int64)
+    lens = np.array([size, 10, 490, 500, size - 7], dtype=np.int64)
+    for algo in (ck.CRC32C, ck.CRC32):
+        got = ck.crc_batch(algo, base, torch.from_numpy(offs).to(gpu), torch.from_numpy(lens.astype(np.int32)).to(gpu),
+                           sync_check=True).cpu().numpy().view(np.uint32)
+        assert (got == oracle.batch(algo, host, offs, lens)).all()
+    h = ck.GpuIntHash()
+    assert (h.resume(5, base, 3, size - 3) & 0xFFFFFFFF) == oracle.resume(0, 5, host[3:size])
+
+
+@pytest.mark.parametrize("mis", [1, 5, 15])
+def test_plan_misaligned_base_pointer(gpu, mis):
+    """The plan aligns chunk ends to absolute device addresses; a base pointer that is not
+    16-byte aligned shifts that grid (PlanGeo.mis) and must not change any digest."""
+    import torch
+    ck.set_plan_mode(2)
+    rng = np.random.default_rng(mis)
+    size = 600_000
+    data = oracle.fill_splitmix64(size + 16, 31)
+    big = _dev_bytes(torch, data, gpu)
+    base = big[mis:mis + size]
+    host = data[mis:mis + size]
+    n = 700
+    lens = rng.integers(0, 20000, n)
+    lens[:40] = np.arange(40)
+    offs = np.array([rng.integers(0, size - l + 1) for l in lens], dtype=np.int64)
+    seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    for algo in (ck.CRC32C, ck.CRC32):
+        got = ck.crc_batch(algo, base, torch.from_numpy(offs).to(gpu), torch.from_numpy(lens.astype(np.int32)).to(gpu),
+                           seeds=torch.from_numpy(seeds.view(np.int32)).to(gpu), sync_check=True)
+        assert (got.cpu().numpy().view(np.uint32) == oracle.batch(algo, host, offs, lens, seeds=seeds)).all()

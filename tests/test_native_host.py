@@ -11,7 +11,7 @@ import oracle
 from bookkeeper_amd import _native
 from bookkeeper_amd import checksum as ck
 from bookkeeper_amd.build import LIB
-from kernel_model import KernelModel
+from kernel_model import KernelModel, plan_model
 
 
 def test_library_exports_every_declared_symbol():
@@ -47,8 +47,11 @@ def test_host_tables_against_oracle(algo):
     L = _native.lib()
     for lanes in (4, 8, 16, 32, 64):
         t = ck.host_tables(algo, lanes)
-        assert t.size == (2 + int(np.log2(lanes))) * 1024 + 256
-        assert (t[-256:] == oracle.table(algo)).all()  # ReflectedIntCrc.java:30-35
+        bo = (2 + int(np.log2(lanes))) * 1024
+        assert t.size == bo + 256 + 2048
+        assert (t[bo:bo + 256] == oracle.table(algo)).all()  # ReflectedIntCrc.java:30-35
+        for off, k in ((bo + 256, 8), (bo + 1280, 12)):  # x^64, x^96 operators
+            assert t[off + 256 * 2 + 7] == oracle.gf_mul(algo, 7 << 16, oracle.xpow8n(algo, k))
         # main operator C = x^(128*lanes): every byte table entry is (b << 8t) * C mod P
         C = oracle.xpow8n(algo, 16 * lanes)
         for tb in range(4):
@@ -81,3 +84,18 @@ def test_group_lane_policy():
     assert L.bkd_get_group_lanes(0, 4096) in (4, 8, 16)
     with pytest.raises(_native.BkdError):
         ck.set_group_lanes(3)
+
+
+@pytest.mark.parametrize("algo", [0, 1])
+def test_plan_chunk_combine_model(algo):
+    """The plan's end-aligned chunking + X = x^(8*CH) Horner combine reproduces the oracle."""
+    tabs = ck.host_tables(algo, 4)
+    rng = np.random.default_rng(algo + 10)
+    jc = 4  # CH = 256 B so that small inputs span many chunks
+    for n in [0, 1, 15, 16, 17, 31, 32, 33, 255, 256, 257, 270, 271, 272, 511, 512, 513, 527, 1000, 1283]:
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        seed = int(rng.integers(0, 2**32))
+        for mis in (0, 1, 7, 15):
+            got = plan_model(tabs, lambda nb: oracle.xpow8n(algo, nb), lambda a, b: oracle.gf_mul(algo, a, b), d,
+                             seed, lanes=4, jc=jc, mis=mis)
+            assert got == oracle.resume(algo, seed, d), (n, mis)
