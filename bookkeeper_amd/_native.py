@@ -65,6 +65,7 @@ PROTOTYPES = {
     "bkd_set_group_lanes": (_int, [_int]),
     "bkd_set_plan_mode": (_int, [_int]),
     "bkd_set_plan_geometry": (_int, [_int, _int, _int]),
+    "bkd_set_plan_prefetch": (_int, [_int]),
     "bkd_get_group_lanes": (_int, [_int, _u64]),
 }
 

@@ -58,9 +58,10 @@ std::atomic<int> g_plan_mode{0};  // 0 auto, 1 direct (one entry per group), 2 c
 
 // Chunked plan geometry (bkd_set_plan_geometry): lanes per group, steps per full chunk
 // (CH = 16 * lanes * jc bytes) and the head-merge threshold in bytes.
-std::atomic<int> g_plan_lanes{8};
-std::atomic<int> g_plan_jc{32};
+std::atomic<int> g_plan_lanes{16};
+std::atomic<int> g_plan_jc{16};
 std::atomic<int> g_plan_merge{16};
+std::atomic<int> g_plan_pf{2};  // loads in flight per lane in the chunk kernel (2, 4 or 8)
 // Indexed batches whose base buffer is at most this size skip the plan (latency over balance).
 constexpr uint64_t kDirectMaxBytes = 256u << 10;
 
@@ -185,8 +186,16 @@ int dispatch_lanes(DeviceState& ds, int lanes, int algo, const uint8_t* base, co
 template <int G>
 void launch_plan_chunks(const uint8_t* base, const bkd::PlanDesc* descs, const uint32_t* count, const uint32_t* tab,
                         uint32_t* out, uint32_t* partials, int blocks, hipStream_t st) {
-    hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, kPF, kNT>), dim3((unsigned)blocks), dim3(bkd::kBlock), 0, st,
-                       base, descs, count, tab, out, partials);
+    const int pf = g_plan_pf.load();
+    if (pf == 8)
+        hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 8, kNT>), dim3((unsigned)blocks), dim3(bkd::kBlock), 0, st,
+                           base, descs, count, tab, out, partials);
+    else if (pf == 4)
+        hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 4, kNT>), dim3((unsigned)blocks), dim3(bkd::kBlock), 0, st,
+                           base, descs, count, tab, out, partials);
+    else
+        hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 2, kNT>), dim3((unsigned)blocks), dim3(bkd::kBlock), 0, st,
+                           base, descs, count, tab, out, partials);
 }
 
 // Indexed batch through the chunked plan (plan_kernels.hpp). Scratch is stream-ordered.
@@ -235,7 +244,9 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
         switch (G) {
             case 4: launch_plan_chunks<4>(base, descs, hdr + bkd::kHdrWork, tab, out, partials, ds.cus, st); break;
             case 8: launch_plan_chunks<8>(base, descs, hdr + bkd::kHdrWork, tab, out, partials, ds.cus, st); break;
-            default: launch_plan_chunks<16>(base, descs, hdr + bkd::kHdrWork, tab, out, partials, ds.cus, st); break;
+            case 16: launch_plan_chunks<16>(base, descs, hdr + bkd::kHdrWork, tab, out, partials, ds.cus, st); break;
+            case 32: launch_plan_chunks<32>(base, descs, hdr + bkd::kHdrWork, tab, out, partials, ds.cus, st); break;
+            default: launch_plan_chunks<64>(base, descs, hdr + bkd::kHdrWork, tab, out, partials, ds.cus, st); break;
         }
         const uint32_t* btab = tab + bkd::gf2::byte_table_offset(G);
         hipLaunchKernelGGL(bkd::plan_combine_kernel, dim3((unsigned)((n + 1023) / 1024)), dim3(1024), 0, st, base,
@@ -307,8 +318,15 @@ int bkd_set_plan_mode(int mode) {
     return BKD_OK;
 }
 
+int bkd_set_plan_prefetch(int loads_in_flight) {
+    if (loads_in_flight != 2 && loads_in_flight != 4 && loads_in_flight != 8)
+        return fail(BKD_ERR_INVALID_ARG, "prefetch depth must be 2, 4 or 8");
+    g_plan_pf.store(loads_in_flight);
+    return BKD_OK;
+}
+
 int bkd_set_plan_geometry(int lanes, int steps_per_chunk, int merge_bytes) {
-    if (lanes != 4 && lanes != 8 && lanes != 16) return fail(BKD_ERR_INVALID_ARG, "plan lanes must be 4, 8 or 16");
+    if (lane_index(lanes) < 0) return fail(BKD_ERR_INVALID_ARG, "plan lanes must be 4, 8, 16, 32 or 64");
     if (steps_per_chunk < 1) return fail(BKD_ERR_INVALID_ARG, "steps_per_chunk must be >= 1");
     const uint32_t step = 16u * (uint32_t)lanes, ch = step * (uint32_t)steps_per_chunk;
     if (ch > 32768u) return fail(BKD_ERR_INVALID_ARG, "chunk size must be <= 32 KiB");

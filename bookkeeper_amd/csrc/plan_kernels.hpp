@@ -27,7 +27,7 @@
 namespace bkd {
 
 constexpr int kPlanBlock = 1024;
-constexpr int kMaxJC = 128;  // bins 0 .. jc + merge steps
+constexpr int kMaxJC = 256;  // bins 0 .. jc + merge steps
 constexpr uint32_t kEmitMax = 64;  // an emit thread writes at most this many full-chunk descriptors
 
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;  // single aligned chunk, no tail: the chunk writes out[] itself

@@ -346,3 +346,30 @@ def test_plan_misaligned_base_pointer(gpu, mis):
         got = ck.crc_batch(algo, base, torch.from_numpy(offs).to(gpu), torch.from_numpy(lens.astype(np.int32)).to(gpu),
                            seeds=torch.from_numpy(seeds.view(np.int32)).to(gpu), sync_check=True)
         assert (got.cpu().numpy().view(np.uint32) == oracle.batch(algo, host, offs, lens, seeds=seeds)).all()
+
+
+@pytest.mark.parametrize("geom", [(4, 64, 16), (4, 16, 512), (16, 8, 16), (8, 32, 4096), (16, 32, 100), (8, 1, 16),
+                                  (32, 8, 16), (64, 4, 300)])
+def test_plan_geometries(gpu, geom):
+    """Every plan geometry (lanes, steps per chunk, head-merge threshold) gives the oracle's digests."""
+    import torch
+    ck.set_plan_mode(2)
+    ck.set_plan_geometry(*geom)
+    try:
+        rng = np.random.default_rng(sum(geom))
+        size = 2_000_000
+        data = oracle.fill_splitmix64(size + 16, 41)
+        big = _dev_bytes(torch, data, gpu)
+        base = big[3:3 + size]
+        host = data[3:3 + size]
+        n = 900
+        lens = rng.integers(0, 40000, n)
+        lens[:64] = np.arange(64) * 7
+        offs = np.array([rng.integers(0, size - l + 1) for l in lens], dtype=np.int64)
+        seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        got = ck.crc_batch(ck.CRC32C, base, torch.from_numpy(offs).to(gpu),
+                           torch.from_numpy(lens.astype(np.int32)).to(gpu),
+                           seeds=torch.from_numpy(seeds.view(np.int32)).to(gpu), sync_check=True)
+        assert (got.cpu().numpy().view(np.uint32) == oracle.batch(0, host, offs, lens, seeds=seeds)).all()
+    finally:
+        ck.set_plan_geometry()
