@@ -399,8 +399,154 @@ struct __attribute__((aligned(16))) PlanDesc {
     uint32_t dst;
 };
 
-// One chunk per group, descriptors read one round ahead (prefetch) so the next chunk's
-// geometry is in registers when the current chunk finishes.
+// ---- pipelined chunk processing for the plan -------------------------------------------
+// A chunk's first PF+1 steps are loaded while the PREVIOUS chunk of the group is still being
+// folded and finalised, so a group never waits a full HBM latency at a chunk boundary. Two
+// register sets (X, Y) alternate between consecutive chunks: the loads for chunk k+1 land in the
+// set chunk k is not using, and no register copy (which would force a vmcnt wait) is needed.
+
+struct ChunkGeo {
+    int64_t s;    // first byte
+    int64_t a;    // this lane's step-0 address (16-byte aligned)
+    int64_t la0;  // step-0 load address: a, or the aligned block holding s for lanes before s
+    uint32_t J;   // steps
+    uint32_t r0;  // register folded into the first bytes
+    uint32_t dst;
+    uint32_t len;
+};
+
+template <int G>
+__device__ __forceinline__ ChunkGeo chunk_geo(const PlanDesc& d, int g) {
+    ChunkGeo c;
+    c.s = (int64_t)(d.s_len & 0xFFFFFFFFFFFFull);
+    c.len = (uint32_t)(d.s_len >> 48);
+    const int64_t e = c.s + (int64_t)c.len;
+    c.J = (uint32_t)((c.len + Geo<G>::kStep - 1) / Geo<G>::kStep);
+    c.a = e - (int64_t)c.J * Geo<G>::kStep + 16 * g;
+    c.la0 = c.a < c.s ? c.a + ((c.s - c.a) & ~(int64_t)15) : c.a;
+    c.r0 = d.r0;
+    c.dst = d.dst;
+    return c;
+}
+
+// Loads of step 0 and steps 1..PF of chunk c (addresses past the chunk clamp to a valid block).
+template <int G, int PF, bool NT>
+__device__ __forceinline__ void chunk_prefetch(const uint8_t* __restrict__ base, const ChunkGeo& c, u32x4& W0,
+                                               u32x4 (&A)[PF]) {
+    W0 = ld16<NT>(base + c.la0);
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {
+        const int64_t addr = (uint32_t)(k + 1) < c.J ? c.a + (int64_t)(k + 1) * Geo<G>::kStep : c.la0;
+        A[k] = ld16<NT>(base + addr);
+    }
+}
+
+// Folds chunk `c` (its W0/A already loaded) and, once its own loads are all issued, prefetches
+// chunk `nx` into NW0/NA. Returns the chunk's raw register (valid in lane g == 0).
+template <int G, int PF, bool NT>
+__device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lanereg, int g,
+                                               const uint8_t* __restrict__ base, const ChunkGeo& c, u32x4 W0,
+                                               u32x4 (&A)[PF], u32x4 (&B)[PF], const ChunkGeo& nx, u32x4& NW0,
+                                               u32x4 (&NA)[PF]) {
+    using Gm = Geo<G>;
+    const int64_t s = c.s, a = c.a;
+    u32x4 w;
+    if (a >= s) w = W0;
+    else if (a + 16 > s) w = mask_low_bytes(W0, (uint32_t)(s - a));
+    else w = u32x4{0u, 0u, 0u, 0u};
+    const uint32_t r0 = c.r0;
+    if (a < s + 4 && a + 16 > s) {
+        const int64_t d = s - a;
+        w.x ^= place_seed(r0, d);
+        w.y ^= place_seed(r0, d - 4);
+        w.z ^= place_seed(r0, d - 8);
+        w.w ^= place_seed(r0, d - 12);
+    }
+    uint32_t fx = 0u;
+    if (a + Gm::kStep < s + 4) fx = place_seed(r0, s - (a + Gm::kStep));
+    uint32_t c0 = w.x, c1 = w.y, c2 = w.z, c3 = w.w;
+    const uint32_t rem = c.J - 1u;
+#define BKD_FOLD0(d)                                     \
+    do {                                                 \
+        c0 = mul_main(lds, c0, lanereg) ^ (d).x ^ fx;    \
+        fx = 0u;                                         \
+        c1 = mul_main(lds, c1, lanereg) ^ (d).y;         \
+        c2 = mul_main(lds, c2, lanereg) ^ (d).z;         \
+        c3 = mul_main(lds, c3, lanereg) ^ (d).w;         \
+    } while (0)
+#define BKD_FOLD(d)                                  \
+    do {                                             \
+        c0 = mul_main(lds, c0, lanereg) ^ (d).x;     \
+        c1 = mul_main(lds, c1, lanereg) ^ (d).y;     \
+        c2 = mul_main(lds, c2, lanereg) ^ (d).z;     \
+        c3 = mul_main(lds, c3, lanereg) ^ (d).w;     \
+    } while (0)
+    if (rem <= (uint32_t)PF) {
+        chunk_prefetch<G, PF, NT>(base, nx, NW0, NA);
+        if (rem > 0u) BKD_FOLD0(A[0]);
+#pragma unroll
+        for (int k = 1; k < PF; ++k)
+            if ((uint32_t)k < rem) BKD_FOLD(A[k]);
+    } else {
+        const uint8_t* p = base + a + (int64_t)(PF + 1) * Gm::kStep;  // first step not yet loaded
+        uint32_t left = rem - (uint32_t)PF;
+        bool first = true;
+        while (left >= 2u * PF) {
+#pragma unroll
+            for (int k = 0; k < PF; ++k) B[k] = ld16<NT>(p + (int64_t)k * Gm::kStep);
+            if (first) BKD_FOLD0(A[0]);
+            else BKD_FOLD(A[0]);
+            first = false;
+#pragma unroll
+            for (int k = 1; k < PF; ++k) BKD_FOLD(A[k]);
+#pragma unroll
+            for (int k = 0; k < PF; ++k) A[k] = ld16<NT>(p + (int64_t)(PF + k) * Gm::kStep);
+#pragma unroll
+            for (int k = 0; k < PF; ++k) BKD_FOLD(B[k]);
+            p += (int64_t)(2 * PF) * Gm::kStep;
+            left -= 2u * PF;
+        }
+#pragma unroll
+        for (int k = 0; k < PF; ++k)
+            if ((uint32_t)k < left) B[k] = ld16<NT>(p + (int64_t)k * Gm::kStep);
+        if (first) BKD_FOLD0(A[0]);
+        else BKD_FOLD(A[0]);
+#pragma unroll
+        for (int k = 1; k < PF; ++k) BKD_FOLD(A[k]);
+#pragma unroll
+        for (int k = 0; k < PF; ++k)
+            if ((uint32_t)(PF + k) < left) A[k] = ld16<NT>(p + (int64_t)(PF + k) * Gm::kStep);
+        chunk_prefetch<G, PF, NT>(base, nx, NW0, NA);  // issued after every load of this chunk
+#pragma unroll
+        for (int k = 0; k < PF; ++k)
+            if ((uint32_t)k < left) BKD_FOLD(B[k]);
+#pragma unroll
+        for (int k = 0; k < PF; ++k)
+            if ((uint32_t)(PF + k) < left) BKD_FOLD(A[k]);
+    }
+#undef BKD_FOLD
+#undef BKD_FOLD0
+    uint32_t v;
+    if constexpr (Gm::kFast) {
+        v = mul_aux(lds, Gm::kX96Off, c0) ^ mul_aux(lds, Gm::kX64Off, c1) ^ mul_aux(lds, Gm::kX32Off, c2) ^ c3;
+        v = lane_tree_dpp<0, Gm::kLevels>(lds, Gm::kX32Off, v);
+    } else {
+        v = mul_aux(lds, Gm::kX32Off, c0) ^ c1;
+        v = mul_aux(lds, Gm::kX32Off, v) ^ c2;
+        v = mul_aux(lds, Gm::kX32Off, v) ^ c3;
+#pragma unroll
+        for (int lv = 0; lv < Gm::kLevels; ++lv) {
+            const uint32_t other = (uint32_t)__shfl_xor((int)v, 1 << lv);
+            v = mul_aux(lds, Gm::kX32Off + 4096u * (uint32_t)(1 + lv), v) ^ other;
+        }
+    }
+    return mul_aux(lds, Gm::kX32Off, v);
+}
+
+// Chunk kernel of the ragged-batch plan: one chunk per group, grid stride over the descriptor
+// list (sorted by step count, plan_kernels.hpp). Descriptors are read two rounds ahead and each
+// chunk's first loads are issued during the previous chunk (chunk_fold), X/Y register sets
+// alternating.
 template <int G, int PF, bool NT>
 __global__ void __launch_bounds__(kBlock) crc_plan_chunks_kernel(const uint8_t* __restrict__ base,
                                                                  const PlanDesc* __restrict__ descs,
@@ -419,18 +565,54 @@ __global__ void __launch_bounds__(kBlock) crc_plan_chunks_kernel(const uint8_t* 
     const uint64_t gid = (uint64_t)blockIdx.x * (kBlock / G) + (uint64_t)(threadIdx.x / G);
     const uint64_t n = *count;
     if (gid >= n) return;
-    PlanDesc nx = descs[gid];
-    for (uint64_t i = gid; i < n; i += ngroups) {
-        const PlanDesc d = nx;
-        const uint64_t ni = i + ngroups < n ? i + ngroups : i;  // unconditional, clamped prefetch
-        nx = descs[ni];
-        const int64_t s = (int64_t)(d.s_len & 0xFFFFFFFFFFFFull);
-        const int64_t len = (int64_t)(d.s_len >> 48);
-        if (len == 0) continue;
-        const uint32_t v = fold_range<G, PF, NT, true>(lds, lanereg, g, base, s, s + len, d.r0);
-        if (g == 0) {
-            if (d.dst & kPlanFinal) out[d.dst & ~kPlanFinal] = ~v;
-            else partials[d.dst] = v;
+
+    auto clampi = [&](uint64_t j) { return j < n ? j : n - 1; };
+    // a hole (len == 0) or a missing next chunk prefetches the current chunk's own blocks
+    auto pf_geo = [&](const ChunkGeo& nx, const ChunkGeo& cur) -> const ChunkGeo& { return nx.len ? nx : cur; };
+    auto emit = [&](const ChunkGeo& c, uint32_t v) {
+        if (g == 0 && c.len) {
+            if (c.dst & kPlanFinal) out[c.dst & ~kPlanFinal] = ~v;
+            else partials[c.dst] = v;
+        }
+    };
+
+    u32x4 W0x, Ax[PF], Bx[PF], W0y, Ay[PF], By[PF];
+    uint64_t i = gid;
+    ChunkGeo cur = chunk_geo<G>(descs[i], g);
+    PlanDesc dn = descs[clampi(i + ngroups)];
+    ChunkGeo safe = cur;
+    if (!cur.len) safe.la0 = safe.a = 0, safe.J = 1;  // hole first: prefetch base[0..16)
+    chunk_prefetch<G, PF, NT>(base, cur.len ? cur : safe, W0x, Ax);
+    for (;;) {
+        {  // chunk i in set X, prefetch into Y
+            const PlanDesc dnn = descs[clampi(i + 2 * ngroups)];
+            const bool more = i + ngroups < n;
+            ChunkGeo nx = chunk_geo<G>(dn, g);
+            if (!more) nx.len = 0;
+            const ChunkGeo& pg = pf_geo(nx, cur.len ? cur : safe);
+            const uint32_t v = cur.len ? chunk_fold<G, PF, NT>(lds, lanereg, g, base, cur, W0x, Ax, Bx, pg, W0y, Ay)
+                                       : (chunk_prefetch<G, PF, NT>(base, pg, W0y, Ay), 0u);
+            emit(cur, v);
+            if (!more) break;
+            i += ngroups;
+            if (cur.len) safe = cur;
+            cur = nx;
+            dn = dnn;
+        }
+        {  // chunk i in set Y, prefetch into X
+            const PlanDesc dnn = descs[clampi(i + 2 * ngroups)];
+            const bool more = i + ngroups < n;
+            ChunkGeo nx = chunk_geo<G>(dn, g);
+            if (!more) nx.len = 0;
+            const ChunkGeo& pg = pf_geo(nx, cur.len ? cur : safe);
+            const uint32_t v = cur.len ? chunk_fold<G, PF, NT>(lds, lanereg, g, base, cur, W0y, Ay, By, pg, W0x, Ax)
+                                       : (chunk_prefetch<G, PF, NT>(base, pg, W0x, Ax), 0u);
+            emit(cur, v);
+            if (!more) break;
+            i += ngroups;
+            if (cur.len) safe = cur;
+            cur = nx;
+            dn = dnn;
         }
     }
 }
