@@ -3,7 +3,7 @@
 // Why: a G-lane group walks its work in lockstep with the other groups of its wavefront, so a
 // wave holding Zipf-sized entries runs as long as its longest entry (SURVEY.md §7 "load balance
 // for Zipf sizes"), and packed entries start and end at arbitrary bytes. The plan therefore
-//  * splits every entry [s, e) at ae = the last 16-byte-aligned device address <= e: the <= 15
+//  * splits every entry [s, e) at ae = the last 128-byte-aligned device address <= e: the <= 127
 //    tail bytes [ae, e) are folded serially by plan_combine_kernel, everything before ae is cut
 //    into chunks of CH = 16*G*JC bytes whose ends are aligned (c = 0 ends at ae, c = m-1 is the
 //    head and starts at s, carrying the seed), so every 16-byte load of the main kernel is an
@@ -71,7 +71,9 @@ __device__ __forceinline__ EntryPlan plan_entry(uint64_t o, uint32_t l, uint64_t
     }
     p.s = (int64_t)o;
     p.e = (int64_t)(o + l);
-    const uint32_t delta = (uint32_t)((pg.mis + (uint64_t)p.e) & 15u);
+    // chunk ends sit on 128-byte lines: a line is then never split between two chunks that run
+    // at different times (each would fetch it from HBM); the <= 127 tail bytes go to the combine
+    const uint32_t delta = (uint32_t)((pg.mis + (uint64_t)p.e) & 127u);
     p.ae = p.e - delta;
     if (p.ae - p.s < 16) {
         p.kind = 1;
@@ -309,16 +311,20 @@ __global__ void plan_combine_kernel(const uint8_t* __restrict__ base, const uint
     }
     const EntryPlan p = plan_entry(o, l, size, pg);
     const uint32_t nq = (uint32_t)(p.e - p.ae);
-    // the tail [ae, e) lies in the aligned 16-byte block at ae: one vector load, no over-read past it
-    const u32x4 tail = nq ? *reinterpret_cast<const u32x4*>(base + p.ae) : u32x4{0u, 0u, 0u, 0u};
     uint32_t reg = partials[slot + p.m - 1u];
     for (int c = (int)p.m - 2; c >= 0; --c) {
         reg = X[reg & 0xffu] ^ X[256 + ((reg >> 8) & 0xffu)] ^ X[512 + ((reg >> 16) & 0xffu)] ^ X[768 + (reg >> 24)];
         reg ^= partials[slot + (uint32_t)c];
     }
-    for (uint32_t k = 0; k < nq; ++k) {
-        const uint32_t w = k < 4 ? tail.x : k < 8 ? tail.y : k < 12 ? tail.z : tail.w;
-        reg = B[(reg ^ (w >> (8 * (k & 3)))) & 0xffu] ^ (reg >> 8);
+    // the tail [ae, e) lies in the 128-byte line at ae: 16-byte vector loads, never past that line
+    const u32x4* tq = reinterpret_cast<const u32x4*>(base + p.ae);
+    for (uint32_t b0 = 0; b0 < nq; b0 += 16) {
+        const u32x4 t = tq[b0 >> 4];
+        const uint32_t nb = nq - b0 < 16u ? nq - b0 : 16u;
+        for (uint32_t k = 0; k < nb; ++k) {
+            const uint32_t w = k < 4 ? t.x : k < 8 ? t.y : k < 12 ? t.z : t.w;
+            reg = B[(reg ^ (w >> (8 * (k & 3)))) & 0xffu] ^ (reg >> 8);
+        }
     }
     out[i] = ~reg;
 }

@@ -84,7 +84,7 @@ class KernelModel:
 
 
 def plan_model(tables_by_lanes, algo_xpow8n, gf_mul, data: bytes, seed: int, lanes: int = 8, jc: int = 32,
-               mis: int = 0) -> int:
+               mis: int = 0) -> int:  # mis: entry start address modulo 128
     """Models the ragged-batch plan (plan_kernels.hpp) for one entry starting at a device address
     congruent to `mis` (mod 16): the aligned part [0, ae) is cut into chunks of CH = 16*lanes*jc bytes
     ending at aligned addresses (head chunk carries the seed; a head < 16 B merges into its
@@ -100,7 +100,7 @@ def plan_model(tables_by_lanes, algo_xpow8n, gf_mul, data: bytes, seed: int, lan
             reg = int(byte[(reg ^ b) & 0xFF]) ^ (reg >> 8)
         return reg
 
-    ae = n - ((mis + n) & 15)
+    ae = n - ((mis + n) & 127)
     if ae < 16:
         return (~serial((~seed) & 0xFFFFFFFF, data)) & 0xFFFFFFFF
     m = (ae + ch - 1) // ch

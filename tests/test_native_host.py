@@ -95,7 +95,7 @@ def test_plan_chunk_combine_model(algo):
     for n in [0, 1, 15, 16, 17, 31, 32, 33, 255, 256, 257, 270, 271, 272, 511, 512, 513, 527, 1000, 1283]:
         d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
         seed = int(rng.integers(0, 2**32))
-        for mis in (0, 1, 7, 15):
+        for mis in (0, 1, 7, 15, 100, 127):
             got = plan_model(tabs, lambda nb: oracle.xpow8n(algo, nb), lambda a, b: oracle.gf_mul(algo, a, b), d,
                              seed, lanes=4, jc=jc, mis=mis)
             assert got == oracle.resume(algo, seed, d), (n, mis)
