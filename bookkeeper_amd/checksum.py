@@ -224,7 +224,7 @@ def set_plan_prefetch(loads_in_flight: int = 2) -> None:
     check(lib().bkd_set_plan_prefetch(loads_in_flight))
 
 
-def set_plan_geometry(lanes: int = 16, steps_per_chunk: int = 16, merge_bytes: int = 16) -> None:
+def set_plan_geometry(lanes: int = 8, steps_per_chunk: int = 32, merge_bytes: int = 16) -> None:
     check(lib().bkd_set_plan_geometry(lanes, steps_per_chunk, merge_bytes))
 
 

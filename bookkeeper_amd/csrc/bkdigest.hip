@@ -58,8 +58,8 @@ std::atomic<int> g_plan_mode{0};  // 0 auto, 1 direct (one entry per group), 2 c
 
 // Chunked plan geometry (bkd_set_plan_geometry): lanes per group, steps per full chunk
 // (CH = 16 * lanes * jc bytes) and the head-merge threshold in bytes.
-std::atomic<int> g_plan_lanes{16};
-std::atomic<int> g_plan_jc{16};
+std::atomic<int> g_plan_lanes{8};
+std::atomic<int> g_plan_jc{32};
 std::atomic<int> g_plan_merge{16};
 std::atomic<int> g_plan_pf{2};  // loads in flight per lane in the chunk kernel (2, 4 or 8)
 // Indexed batches whose base buffer is at most this size skip the plan (latency over balance).

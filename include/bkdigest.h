@@ -154,7 +154,7 @@ int bkd_set_group_lanes(int lanes);
 int bkd_set_plan_mode(int mode);
 /* Chunked-plan geometry: lanes per group (4, 8, 16, 32 or 64), steps per full chunk (chunk = 16 * lanes *
  * steps bytes, <= 32 KiB) and the head-merge threshold in bytes (a head chunk shorter than this
- * joins its neighbour; >= 16). Default 16, 16, 16 (4 KiB chunks). */
+ * joins its neighbour; >= 16). Default 8, 32, 16 (4 KiB chunks; tools/tune_plan.py). */
 int bkd_set_plan_geometry(int lanes, int steps_per_chunk, int merge_bytes);
 /* Register double-buffer depth of the plan's chunk kernel (2, 4 or 8 loads per lane). */
 int bkd_set_plan_prefetch(int loads_in_flight);
