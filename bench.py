@@ -59,6 +59,24 @@ def _splitmix_words(nwords: int, seed: int) -> bytes:
     return z.tobytes()
 
 
+def shard_first_word(rank: int, entries_per_rank: int, entry_len: int) -> int:
+    """The job's input is ONE global splitmix64 stream; rank r owns entries
+    [r*entries_per_rank, (r+1)*entries_per_rank), i.e. stream words from this index on."""
+    assert (entries_per_rank * entry_len) % 8 == 0
+    return rank * entries_per_rank * entry_len // 8
+
+
+def max_over_ranks(value: float, device=None) -> float:
+    """Whole-job time = the slowest rank's (all_reduce MAX; the only cross-rank traffic)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(value)
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def cpu_baseline(host_sample: np.ndarray, entry_len: int, algo: int = 0, budget_s: float = 8.0):
     """Reference circe crc32c() (oracle/_ref) over a bounded sample, all host cores we may use."""
     import oracle
@@ -111,6 +129,8 @@ def main() -> None:
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--zipf-align", type=int, default=1, help="diagnostic: align Zipf entries")
     ap.add_argument("--plan-mode", type=int, default=0, help="0 auto, 1 direct, 2 chunked plan")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL) on a real node; gloo only to rehearse several ranks on one GPU")
     args = ap.parse_args()
 
     import torch
@@ -124,10 +144,16 @@ def main() -> None:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a HIP device (no CPU path exists)")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and local >= ndev:
+        raise SystemExit(f"LOCAL_RANK {local} but only {ndev} visible GPUs")
+    dev = torch.device("cuda", local % ndev)  # % only matters for a gloo rehearsal on fewer GPUs
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     algo = ck.CRC32C if args.algo == "crc32c" else ck.CRC32
     ck.set_group_lanes(args.lanes)
     ck.set_plan_mode(args.plan_mode)
@@ -138,7 +164,7 @@ def main() -> None:
         n = args.entries or (1 << 20 if args.config == "uniform4k" else 8 << 20)
         base = torch.empty(n * entry_len, dtype=torch.uint8, device=dev)
         # the job's data is ONE global splitmix64 stream; rank r holds its slice
-        ck.fill_splitmix64(base, 42, first_word=rank * n * entry_len // 8)
+        ck.fill_splitmix64(base, 42, first_word=shard_first_word(rank, n, entry_len))
         out = torch.empty(n, dtype=torch.int32, device=dev)
         payload_bytes = n * entry_len
         algo_bytes = n * (entry_len + 4)  # read payload + write u32 digest
@@ -189,10 +215,7 @@ def main() -> None:
     kernel_ms = [a.elapsed_time(b) for a, b in ev]
     avg_kernel_s = float(np.mean(kernel_ms)) / 1e3
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed_max = float(t.item())
+    elapsed_max = max_over_ranks(elapsed, dev if args.dist_backend == "nccl" else None)
 
     total_payload = payload_bytes * world * args.steps  # every rank processes its batch once per step
     value = total_payload / elapsed_max / GIB

@@ -1,0 +1,70 @@
+"""CPU rehearsal of the N>1 path with a world_size-2 gloo group (127.0.0.1).
+
+The GPU path shards entries across ranks with no data-path collective. Here each
+rank builds its shard of the global splitmix64 stream exactly as bench.py does
+(shard_first_word), digests it with the oracle as a CPU stand-in for its GPU, and rank 0 checks
+that the concatenated per-rank digests equal the digests of the unsharded batch; max_over_ranks
+(the only collective bench.py uses) is checked too."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n_per_rank, entry_len, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch
+    import torch.distributed as dist
+    import oracle
+    from bench import max_over_ranks, shard_first_word
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        fw = shard_first_word(rank, n_per_rank, entry_len)
+        shard = oracle.fill_splitmix64(n_per_rank * entry_len, 42, fw)
+        crcs = oracle.uniform(oracle.CRC32C, shard, entry_len, entry_len, n_per_rank)
+        gathered = [torch.zeros(n_per_rank, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(gathered, torch.from_numpy(crcs.astype(np.int64)))
+        slowest = max_over_ranks(0.25 * (rank + 1))
+        if rank == 0:
+            q.put((np.concatenate([g.numpy() for g in gathered]).astype(np.uint32), slowest))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_digests_equal_unsharded(world):
+    n_per_rank, entry_len = 512, 4096
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_per_rank, entry_len, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got, slowest = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    import oracle
+    whole = oracle.fill_splitmix64(world * n_per_rank * entry_len, 42)
+    want = oracle.uniform(oracle.CRC32C, whole, entry_len, entry_len, world * n_per_rank)
+    assert (got == want).all()
+    assert slowest == pytest.approx(0.25 * world)
+
+
+def test_single_process_reduction_is_identity():
+    from bench import max_over_ranks, shard_first_word
+    assert max_over_ranks(1.5) == 1.5
+    assert shard_first_word(3, 1 << 20, 4096) == 3 * (1 << 20) * 512
