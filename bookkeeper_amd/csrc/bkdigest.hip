@@ -281,6 +281,167 @@ bool is_device_pointer(const void* p) {
     return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
 }
 
+// ---- host-memory batches: pinned, double-buffered H2D -> kernel -> D2H -------------------
+// Entries sorted by offset are cut into segments of at most kSeg payload bytes / kSegEntries
+// entries; segment k uses staging slot k % 2 (its own stream), so the H2D copy of one segment
+// overlaps the kernel and D2H of the other. A pinned (page-locked / registered) source is DMA'd
+// in place; a pageable one is first copied into the slot's pinned buffer by the host.
+struct HostStage {
+    static constexpr size_t kSeg = 64u << 20;
+    static constexpr size_t kSegEntries = 1u << 20;
+    std::mutex mu;
+    bool ready = false;
+    uint8_t* h_pin[2] = {};
+    uint8_t* d_buf[2] = {};
+    uint64_t* h_off[2] = {};
+    uint32_t* h_len[2] = {};
+    uint32_t* h_seed[2] = {};
+    uint32_t* h_res[2] = {};
+    uint64_t* d_off[2] = {};
+    uint32_t* d_len[2] = {};
+    uint32_t* d_seed[2] = {};
+    uint32_t* d_res[2] = {};
+    hipStream_t st[2] = {};
+    hipEvent_t done[2] = {};
+    int init() {
+        if (ready) return BKD_OK;
+        for (int s = 0; s < 2; ++s) {
+            BKD_HIP(hipHostMalloc((void**)&h_pin[s], kSeg, hipHostMallocDefault));
+            BKD_HIP(hipMalloc((void**)&d_buf[s], kSeg));
+            BKD_HIP(hipHostMalloc((void**)&h_off[s], kSegEntries * 8, hipHostMallocDefault));
+            BKD_HIP(hipHostMalloc((void**)&h_len[s], kSegEntries * 4, hipHostMallocDefault));
+            BKD_HIP(hipHostMalloc((void**)&h_seed[s], kSegEntries * 4, hipHostMallocDefault));
+            BKD_HIP(hipHostMalloc((void**)&h_res[s], kSegEntries * 4, hipHostMallocDefault));
+            BKD_HIP(hipMalloc((void**)&d_off[s], kSegEntries * 8));
+            BKD_HIP(hipMalloc((void**)&d_len[s], kSegEntries * 4));
+            BKD_HIP(hipMalloc((void**)&d_seed[s], kSegEntries * 4));
+            BKD_HIP(hipMalloc((void**)&d_res[s], kSegEntries * 4));
+            BKD_HIP(hipStreamCreateWithFlags(&st[s], hipStreamNonBlocking));
+            BKD_HIP(hipEventCreateWithFlags(&done[s], hipEventDisableTiming));
+        }
+        ready = true;
+        return BKD_OK;
+    }
+};
+HostStage g_stage[kMaxDevices];
+
+int indexed_batch(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, const uint64_t* offsets,
+                  const uint32_t* lengths, uint64_t n, const uint32_t* seeds, uint32_t seed_all, uint32_t* out,
+                  hipStream_t st);
+
+bool is_pinned_host(const void* p) {
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return attr.type == hipMemoryTypeHost;
+}
+
+// Unsorted index or an entry larger than a segment: one device copy of the spanned bytes.
+int host_batch_oneshot(DeviceState& ds, HostStage& hs, int algo, const uint8_t* h_base, uint64_t base_size,
+                       const uint64_t* h_offsets, const uint32_t* h_lengths, uint64_t n, const uint32_t* h_seeds,
+                       uint32_t seed_all, uint32_t* h_out) {
+    hipStream_t st = hs.st[0];
+    uint8_t* d_base = nullptr;
+    uint64_t* d_off = nullptr;
+    uint32_t *d_len = nullptr, *d_seeds = nullptr, *d_out = nullptr;
+    hipError_t e = hipSuccess;
+    if (base_size) e = hipMallocAsync((void**)&d_base, base_size, st);
+    if (e == hipSuccess) e = hipMallocAsync((void**)&d_off, n * 8, st);
+    if (e == hipSuccess) e = hipMallocAsync((void**)&d_len, n * 4, st);
+    if (e == hipSuccess) e = hipMallocAsync((void**)&d_out, n * 4, st);
+    if (e == hipSuccess && h_seeds) e = hipMallocAsync((void**)&d_seeds, n * 4, st);
+    if (e == hipSuccess && base_size) e = hipMemcpyAsync(d_base, h_base, base_size, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_off, h_offsets, n * 8, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_len, h_lengths, n * 4, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess && h_seeds) e = hipMemcpyAsync(d_seeds, h_seeds, n * 4, hipMemcpyHostToDevice, st);
+    int rc = BKD_OK;
+    if (e != hipSuccess) rc = fail(BKD_ERR_HIP, std::string("host batch staging: ") + hipGetErrorString(e));
+    if (rc == BKD_OK) rc = indexed_batch(ds, algo, d_base, base_size, d_off, d_len, n, d_seeds, seed_all, d_out, st);
+    if (rc == BKD_OK) {
+        e = hipMemcpyAsync(h_out, d_out, n * 4, hipMemcpyDeviceToHost, st);
+        if (e != hipSuccess) rc = fail(BKD_ERR_HIP, std::string("host batch: ") + hipGetErrorString(e));
+    }
+    for (void* p : {(void*)d_base, (void*)d_off, (void*)d_len, (void*)d_seeds, (void*)d_out})
+        if (p) (void)hipFreeAsync(p, st);
+    e = hipStreamSynchronize(st);
+    if (rc == BKD_OK && e != hipSuccess) rc = fail(BKD_ERR_HIP, std::string("host batch: ") + hipGetErrorString(e));
+    return rc;
+}
+
+int host_batch_pipelined(DeviceState& ds, HostStage& hs, int algo, const uint8_t* h_base, const uint64_t* h_offsets,
+                         const uint32_t* h_lengths, uint64_t n, const uint32_t* h_seeds, uint32_t seed_all,
+                         uint32_t* h_out) {
+    const bool pinned = is_pinned_host(h_base);
+    uint64_t pend_i0[2] = {0, 0}, pend_cnt[2] = {0, 0};
+    bool busy[2] = {false, false};
+    auto drain = [&](int s) -> int {  // wait for slot s and hand its digests back
+        if (!busy[s]) return BKD_OK;
+        BKD_HIP(hipEventSynchronize(hs.done[s]));
+        memcpy(h_out + pend_i0[s], hs.h_res[s], pend_cnt[s] * 4);
+        busy[s] = false;
+        return BKD_OK;
+    };
+    uint64_t i0 = 0;
+    int rc = BKD_OK;
+    for (int k = 0; i0 < n && rc == BKD_OK; ++k) {
+        const int s = k & 1;
+        const uint64_t b0 = h_offsets[i0];
+        uint64_t i1 = i0, b1 = b0;
+        while (i1 < n && i1 - i0 < HostStage::kSegEntries) {
+            const uint64_t e1 = std::max<uint64_t>(b1, h_offsets[i1] + h_lengths[i1]);
+            if (e1 - b0 > HostStage::kSeg && i1 > i0) break;
+            b1 = e1;
+            ++i1;
+        }
+        const uint64_t cnt = i1 - i0, span = b1 - b0;
+        if ((rc = drain(s))) break;
+        if (span > HostStage::kSeg) {  // a single entry larger than a segment (cnt == 1, offset b0)
+            if ((rc = drain(s ^ 1))) break;
+            const uint64_t zero = 0;
+            rc = host_batch_oneshot(ds, hs, algo, h_base + b0, span, &zero, h_lengths + i0, 1,
+                                    h_seeds ? h_seeds + i0 : nullptr, seed_all, h_out + i0);
+            i0 = i1;
+            continue;
+        }
+        for (uint64_t j = 0; j < cnt; ++j) {
+            hs.h_off[s][j] = h_offsets[i0 + j] - b0;
+            hs.h_len[s][j] = h_lengths[i0 + j];
+        }
+        if (h_seeds) memcpy(hs.h_seed[s], h_seeds + i0, cnt * 4);
+        const uint8_t* src = h_base + b0;
+        if (!pinned) {
+            memcpy(hs.h_pin[s], src, span);
+            src = hs.h_pin[s];
+        }
+        hipStream_t st = hs.st[s];
+        hipError_t e = hipMemcpyAsync(hs.d_buf[s], src, span, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(hs.d_off[s], hs.h_off[s], cnt * 8, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(hs.d_len[s], hs.h_len[s], cnt * 4, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess && h_seeds) e = hipMemcpyAsync(hs.d_seed[s], hs.h_seed[s], cnt * 4, hipMemcpyHostToDevice, st);
+        if (e != hipSuccess) {
+            rc = fail(BKD_ERR_HIP, std::string("host batch H2D: ") + hipGetErrorString(e));
+            break;
+        }
+        rc = indexed_batch(ds, algo, hs.d_buf[s], span, hs.d_off[s], hs.d_len[s], cnt, h_seeds ? hs.d_seed[s] : nullptr,
+                           seed_all, hs.d_res[s], st);
+        if (rc) break;
+        e = hipMemcpyAsync(hs.h_res[s], hs.d_res[s], cnt * 4, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipEventRecord(hs.done[s], st);
+        if (e != hipSuccess) {
+            rc = fail(BKD_ERR_HIP, std::string("host batch D2H: ") + hipGetErrorString(e));
+            break;
+        }
+        busy[s] = true;
+        pend_i0[s] = i0;
+        pend_cnt[s] = cnt;
+        i0 = i1;
+    }
+    const int r0 = drain(0), r1 = drain(1);
+    return rc ? rc : (r0 ? r0 : r1);
+}
+
 }  // namespace
 
 extern "C" {
@@ -389,48 +550,25 @@ int bkd_crc_batch_host(int algo, const void* h_base, uint64_t base_size, const u
     if (!valid_algo(algo)) return fail(BKD_ERR_INVALID_ARG, "unknown algorithm");
     if (n == 0) return BKD_OK;
     if (!h_offsets || !h_lengths || !h_out || (!h_base && base_size)) return fail(BKD_ERR_INVALID_ARG, "null buffer");
-    for (uint64_t i = 0; i < n; ++i)
+    bool sorted = true;
+    for (uint64_t i = 0; i < n; ++i) {
         if (h_offsets[i] > base_size || (uint64_t)h_lengths[i] > base_size - h_offsets[i])
             return fail(BKD_ERR_BOUNDS, "entry " + std::to_string(i) + " exceeds base buffer");
+        if (i && h_offsets[i] < h_offsets[i - 1]) sorted = false;
+    }
     DeviceState* ds = nullptr;
     int rc = ensure_current(&ds);
     if (rc) return rc;
-    hipStream_t st;
-    BKD_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    uint8_t* d_base = nullptr;
-    uint64_t* d_off = nullptr;
-    uint32_t *d_len = nullptr, *d_seeds = nullptr, *d_out = nullptr;
-    auto cleanup = [&]() {
-        (void)hipStreamSynchronize(st);
-        if (d_base) (void)hipFree(d_base);
-        if (d_off) (void)hipFree(d_off);
-        if (d_len) (void)hipFree(d_len);
-        if (d_seeds) (void)hipFree(d_seeds);
-        if (d_out) (void)hipFree(d_out);
-        (void)hipStreamDestroy(st);
-    };
-    hipError_t e = hipSuccess;
-    if (base_size) e = hipMalloc(&d_base, base_size);
-    if (e == hipSuccess) e = hipMalloc(&d_off, n * 8);
-    if (e == hipSuccess) e = hipMalloc(&d_len, n * 4);
-    if (e == hipSuccess) e = hipMalloc(&d_out, n * 4);
-    if (e == hipSuccess && h_seeds) e = hipMalloc(&d_seeds, n * 4);
-    if (e == hipSuccess && base_size) e = hipMemcpyAsync(d_base, h_base, base_size, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_off, h_offsets, n * 8, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_len, h_lengths, n * 4, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess && h_seeds) e = hipMemcpyAsync(d_seeds, h_seeds, n * 4, hipMemcpyHostToDevice, st);
-    if (e != hipSuccess) {
-        cleanup();
-        return fail(BKD_ERR_HIP, std::string("host batch staging: ") + hipGetErrorString(e));
-    }
-    rc = indexed_batch(*ds, algo, d_base, base_size, d_off, d_len, n, d_seeds, seed_all, d_out, st);
-    if (rc == BKD_OK) {
-        e = hipMemcpyAsync(h_out, d_out, n * 4, hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
-        if (e != hipSuccess) rc = fail(BKD_ERR_HIP, std::string("host batch: ") + hipGetErrorString(e));
-    }
-    cleanup();
-    return rc;
+    int dev = 0;
+    BKD_HIP(hipGetDevice(&dev));
+    HostStage& hs = g_stage[dev];
+    std::lock_guard<std::mutex> lk(hs.mu);
+    rc = hs.init();
+    if (rc) return rc;
+    if (!sorted) return host_batch_oneshot(*ds, hs, algo, (const uint8_t*)h_base, base_size, h_offsets, h_lengths, n,
+                                           h_seeds, seed_all, h_out);
+    return host_batch_pipelined(*ds, hs, algo, (const uint8_t*)h_base, h_offsets, h_lengths, n, h_seeds, seed_all,
+                                h_out);
 }
 
 int bkd_resume(int algo, uint32_t current, const void* ptr, uint64_t len, uint32_t* out) {

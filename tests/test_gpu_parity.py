@@ -373,3 +373,27 @@ def test_plan_geometries(gpu, geom):
         assert (got.cpu().numpy().view(np.uint32) == oracle.batch(0, host, offs, lens, seeds=seeds)).all()
     finally:
         ck.set_plan_geometry()
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_batch_pipelined_segments(gpu, pinned):
+    """Host-memory batches spanning several 64 MiB staging segments (sorted, packed), one entry
+    larger than a segment, and an unsorted index; pinned and pageable sources."""
+    import torch
+    size = 150 << 20
+    t = torch.empty(size, dtype=torch.uint8, pin_memory=pinned)
+    host = t.numpy()
+    host[:] = oracle.fill_splitmix64(size, 5)
+    rng = np.random.default_rng(int(pinned))
+    lens = rng.integers(0, 300000, 900)
+    lens[450] = 70 << 20  # > one segment
+    offs = np.zeros(lens.size, dtype=np.uint64)
+    np.cumsum(lens[:-1], out=offs[1:])
+    keep = offs + lens <= size
+    offs, lens = offs[keep], lens[keep]
+    seeds = rng.integers(0, 2**32, lens.size, dtype=np.uint64).astype(np.uint32)
+    got = ck.crc_batch_host(ck.CRC32C, host, offs, lens, seeds=seeds)
+    assert (got == oracle.batch(0, host, offs, lens, seeds=seeds)).all()
+    perm = rng.permutation(lens.size)[:200]
+    got = ck.crc_batch_host(ck.CRC32, host, offs[perm], lens[perm])
+    assert (got == oracle.batch(1, host, offs[perm], lens[perm])).all()
