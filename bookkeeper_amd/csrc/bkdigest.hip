@@ -250,7 +250,8 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
         }
         const uint32_t* btab = tab + bkd::gf2::byte_table_offset(G);
         hipLaunchKernelGGL(bkd::plan_combine_kernel, dim3((unsigned)((n + 1023) / 1024)), dim3(1024), 0, st, base,
-                           offsets, lengths, seeds, seed_all, size, n, pg, xtab, btab, pslot, partials, out, ds.err);
+                           offsets, lengths, seeds, seed_all, size, n, pg, xtab, tab + 1024, btab, pslot, partials, out,
+                           ds.err);
         e = hipGetLastError();
         if (e != hipSuccess) rc = fail(BKD_ERR_HIP, std::string("plan kernels: ") + hipGetErrorString(e));
     }

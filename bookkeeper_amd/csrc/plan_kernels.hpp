@@ -283,12 +283,14 @@ __global__ void plan_expand_big_kernel(const uint64_t* __restrict__ offsets, con
 __global__ void plan_combine_kernel(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets,
                                     const uint32_t* __restrict__ lengths, const uint32_t* __restrict__ seeds,
                                     uint32_t seed_all, uint64_t size, uint64_t n, PlanGeo pg,
-                                    const uint32_t* __restrict__ xtab, const uint32_t* __restrict__ btab,
-                                    const uint32_t* __restrict__ pslot, const uint32_t* __restrict__ partials,
+                                    const uint32_t* __restrict__ xtab, const uint32_t* __restrict__ x32tab,
+                                    const uint32_t* __restrict__ btab, const uint32_t* __restrict__ pslot, const uint32_t* __restrict__ partials,
                                     uint32_t* __restrict__ out, uint32_t* __restrict__ err) {
     __shared__ uint32_t X[1024];
+    __shared__ uint32_t W[1024];
     __shared__ uint32_t B[256];
     for (int k = threadIdx.x; k < 1024; k += blockDim.x) X[k] = xtab[k];
+    for (int k = threadIdx.x; k < 1024; k += blockDim.x) W[k] = x32tab[k];
     for (int k = threadIdx.x; k < 256; k += blockDim.x) B[k] = btab[k];
     __syncthreads();
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -305,7 +307,14 @@ __global__ void plan_combine_kernel(const uint8_t* __restrict__ base, const uint
     if (slot == kSerial || slot == kDirect) {
         uint32_t reg = ~(seeds ? seeds[i] : seed_all);
         const uint8_t* q = base + o;
-        for (uint32_t k = 0; k < l; ++k) reg = B[(reg ^ q[k]) & 0xffu] ^ (reg >> 8);
+        const uint8_t* qe = q + l;
+        // bytes up to a 4-byte boundary, aligned dwords by x^32, trailing bytes
+        while (q < qe && ((uintptr_t)q & 3u)) reg = B[(reg ^ *q++) & 0xffu] ^ (reg >> 8);
+        for (; qe - q >= 4; q += 4) {
+            const uint32_t r = reg ^ *reinterpret_cast<const uint32_t*>(q);
+            reg = W[r & 0xffu] ^ W[256 + ((r >> 8) & 0xffu)] ^ W[512 + ((r >> 16) & 0xffu)] ^ W[768 + (r >> 24)];
+        }
+        while (q < qe) reg = B[(reg ^ *q++) & 0xffu] ^ (reg >> 8);
         out[i] = ~reg;
         return;
     }
@@ -316,14 +325,22 @@ __global__ void plan_combine_kernel(const uint8_t* __restrict__ base, const uint
         reg = X[reg & 0xffu] ^ X[256 + ((reg >> 8) & 0xffu)] ^ X[512 + ((reg >> 16) & 0xffu)] ^ X[768 + (reg >> 24)];
         reg ^= partials[slot + (uint32_t)c];
     }
-    // the tail [ae, e) lies in the 128-byte line at ae: 16-byte vector loads, never past that line
+    // the tail [ae, e) lies in the 128-byte line at ae: 16-byte vector loads, never past that line;
+    // whole dwords advance the register by x^32 (4 independent lookups), the last 0-3 bytes by x^8
     const u32x4* tq = reinterpret_cast<const u32x4*>(base + p.ae);
     for (uint32_t b0 = 0; b0 < nq; b0 += 16) {
         const u32x4 t = tq[b0 >> 4];
         const uint32_t nb = nq - b0 < 16u ? nq - b0 : 16u;
-        for (uint32_t k = 0; k < nb; ++k) {
-            const uint32_t w = k < 4 ? t.x : k < 8 ? t.y : k < 12 ? t.z : t.w;
-            reg = B[(reg ^ (w >> (8 * (k & 3)))) & 0xffu] ^ (reg >> 8);
+        const uint32_t nw = nb >> 2;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t w = k == 0 ? t.x : k == 1 ? t.y : k == 2 ? t.z : t.w;
+            if (k < nw) {
+                const uint32_t r = reg ^ w;
+                reg = W[r & 0xffu] ^ W[256 + ((r >> 8) & 0xffu)] ^ W[512 + ((r >> 16) & 0xffu)] ^ W[768 + (r >> 24)];
+            } else if (k == nw) {
+                for (uint32_t j = 0; j < (nb & 3u); ++j) reg = B[(reg ^ (w >> (8 * j))) & 0xffu] ^ (reg >> 8);
+            }
         }
     }
     out[i] = ~reg;
