@@ -58,6 +58,8 @@ PROTOTYPES = {
     "bkd_resume": (_int, [_int, _u32, _vp, _u64, _c.POINTER(_u32)]),
     "bkd_digest_package_batch": (_int, [_int, _i64, _vp, _vp, _vp, _vp, _u64, _vp, _vp, _u64, _vp, _u64, _vp, _vp]),
     "bkd_digest_verify_batch": (_int, [_int, _i64, _i64, _int, _vp, _u64, _vp, _vp, _u64, _vp, _vp, _vp]),
+    "bkd_entrylog_index": (_int, [_vp, _u64, _u64, _vp, _vp, _vp, _u64, _vp, _vp]),
+    "bkd_entrylog_verify": (_int, [_int, _vp, _u64, _vp, _vp, _u64, _vp, _vp, _vp]),
     "bkd_fill_splitmix64": (_int, [_vp, _u64, _u64, _u64, _vp]),
     "bkd_host_tables": (_i64, [_int, _int, _vp, _u64]),
     "bkd_host_gf_mul": (_u32, [_int, _u32, _u32]),

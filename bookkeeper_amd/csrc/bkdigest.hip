@@ -48,6 +48,7 @@ struct DeviceState {
     int cus = 0;
     uint32_t* tables[2][5] = {};  // [algo][lane choice] compact operator images
     uint32_t* err = nullptr;      // sticky bounds-violation flag for indexed batches
+    uint32_t* xinv[2] = {};       // [algo] x^(-8k), k = 0..127: removes the plan's zero padding
     std::map<uint64_t, uint32_t*> xtab;  // (algo, CH) -> x^(8*CH) operator for the plan's combine
 };
 
@@ -91,6 +92,12 @@ int init_device_locked(int dev) {
             BKD_HIP(hipMalloc(&ds.tables[algo][k], img.size() * sizeof(uint32_t)));
             BKD_HIP(hipMemcpy(ds.tables[algo][k], img.data(), img.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
         }
+    }
+    for (int algo = 0; algo < 2; ++algo) {
+        uint32_t inv[128];
+        for (uint32_t k = 0; k < 128; ++k) inv[k] = bkd::gf2::xpow_neg8(algo, k);
+        BKD_HIP(hipMalloc(&ds.xinv[algo], sizeof(inv)));
+        BKD_HIP(hipMemcpy(ds.xinv[algo], inv, sizeof(inv), hipMemcpyHostToDevice));
     }
     // stream-ordered scratch for the plan: keep freed blocks in the pool between calls
     hipMemPool_t pool;
@@ -209,13 +216,14 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     pg.step = 16u * (uint32_t)G;
     pg.jc = (uint32_t)g_plan_jc.load();
     pg.ch = pg.step * pg.jc;
-    pg.mis = (uint32_t)((uintptr_t)base & 15u);
+    pg.mis = (uint32_t)((uintptr_t)base & 127u);
     pg.merge = (uint32_t)g_plan_merge.load();
     pg.nbins = (pg.ch + pg.merge - 1u + pg.step - 1u) / pg.step + 1u;
     const uint32_t* xtab = nullptr;
     int rc = xtab_for(ds, algo, pg.ch, &xtab);
     if (rc) return rc;
-    const uint64_t capacity = std::min<uint64_t>(n + size / pg.ch + 16, 0xFFFFFFF0ull);
+    // non-overlapping entries need at most sum(ceil((len + 127) / CH)) <= n + (size + 127 n) / CH chunks
+    const uint64_t capacity = std::min<uint64_t>(n + (size + 128u * n) / pg.ch + 16, 0xFFFFFFF0ull);
     const uint32_t nb = (uint32_t)((n + bkd::kPlanBlock - 1) / bkd::kPlanBlock);
     const uint32_t ncols = pg.nbins + 1u;
     uint32_t *blk = nullptr, *blkoff = nullptr, *hdr = nullptr, *run_start = nullptr, *pslot = nullptr,
@@ -250,8 +258,8 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
         }
         const uint32_t* btab = tab + bkd::gf2::byte_table_offset(G);
         hipLaunchKernelGGL(bkd::plan_combine_kernel, dim3((unsigned)((n + 1023) / 1024)), dim3(1024), 0, st, base,
-                           offsets, lengths, seeds, seed_all, size, n, pg, xtab, tab + 1024, btab, pslot, partials, out,
-                           ds.err);
+                           offsets, lengths, seeds, seed_all, size, n, pg, xtab, tab + 1024, btab, ds.xinv[algo],
+                           bkd::gf2::poly(algo), pslot, partials, out, ds.err);
         e = hipGetLastError();
         if (e != hipSuccess) rc = fail(BKD_ERR_HIP, std::string("plan kernels: ") + hipGetErrorString(e));
     }
@@ -265,7 +273,8 @@ int indexed_batch(DeviceState& ds, int algo, const uint8_t* base, uint64_t size,
                   const uint32_t* lengths, uint64_t n, const uint32_t* seeds, uint32_t seed_all, uint32_t* out,
                   hipStream_t st) {
     const int mode = g_plan_mode.load();
-    const bool direct = mode == 1 || (mode == 0 && size <= kDirectMaxBytes);
+    // plan descriptors hold 41-bit offsets (PlanDesc): larger buffers take the direct kernel
+    const bool direct = mode == 1 || (mode == 0 && size <= kDirectMaxBytes) || size >= bkd::kPlanMaxSize;
     if (!direct) return launch_plan(ds, algo, base, size, offsets, lengths, n, seeds, seed_all, out, st);
     bkd::IndexedSrc src{n, offsets, lengths, seeds, seed_all, size, out};
     return dispatch_lanes(ds, auto_lanes(n ? size / n : 0), algo, base, src, n, st);
@@ -640,14 +649,17 @@ int bkd_digest_package_batch(int algo, int64_t ledger_id, const int64_t* d_entry
     return BKD_OK;
 }
 
-int bkd_digest_verify_batch(int algo, int64_t ledger_id, int64_t first_entry_id, int skip_entry_check,
-                            const void* d_framed, uint64_t framed_size, const uint64_t* d_offsets,
-                            const uint32_t* d_lengths, uint64_t n, int32_t* d_status, uint64_t* d_first_bad,
-                            void* stream) {
+namespace {
+// Shared by bkd_digest_verify_batch and bkd_entrylog_verify: header CRCs -> payload CRCs seeded
+// with them through the indexed path (chunked plan for large ragged batches) -> compare.
+int verify_framed(int algo, int64_t ledger_id, int64_t first_entry_id, int id_checks, const void* d_framed,
+                  uint64_t framed_size, const uint64_t* d_offsets, const uint32_t* d_lengths, uint64_t n,
+                  int32_t* d_status, uint64_t* d_first_bad, void* stream) {
     if (!valid_algo(algo)) return fail(BKD_ERR_INVALID_ARG, "unknown algorithm");
     const uint32_t mac = algo == BKD_CRC32C ? 4u : 8u;
     if (!d_first_bad) return fail(BKD_ERR_INVALID_ARG, "null first_bad");
     if (n && (!d_offsets || !d_lengths || !d_status)) return fail(BKD_ERR_INVALID_ARG, "null buffer");
+    if (n && !d_framed) return fail(BKD_ERR_INVALID_ARG, "null framed buffer");
     DeviceState* ds = nullptr;
     int rc = ensure_current(&ds);
     if (rc) return rc;
@@ -656,22 +668,97 @@ int bkd_digest_verify_batch(int algo, int64_t ledger_id, int64_t first_entry_id,
         BKD_HIP(hipMemsetAsync(d_first_bad, 0, sizeof(uint64_t), st));
         return BKD_OK;
     }
-    const int lanes = auto_lanes(framed_size / n);
-    const uint32_t* tab = ds->tables[algo][lane_index(lanes)];
-    const uint32_t* btab = tab + bkd::gf2::byte_table_offset(lanes);
+    const uint32_t* btab = ds->tables[algo][lane_index(4)] + bkd::gf2::byte_table_offset(4);
     const unsigned blocks = (unsigned)((n + 255) / 256);
-    uint32_t* scratch = reinterpret_cast<uint32_t*>(d_status);
-    hipLaunchKernelGGL(bkd::verify_header_kernel, dim3(blocks), dim3(256), 0, st, btab, (const uint8_t*)d_framed,
-                       framed_size, d_offsets, d_lengths, n, mac, scratch, d_first_bad);
-    BKD_HIP(hipGetLastError());
-    bkd::FramedPayloadSrc src{n, d_offsets, d_lengths, scratch, framed_size, mac};
-    rc = dispatch_lanes(*ds, lanes, algo, (const uint8_t*)d_framed, src, n, st);
-    if (rc) return rc;
-    hipLaunchKernelGGL(bkd::verify_finish_kernel, dim3(blocks), dim3(256), 0, st, (const uint8_t*)d_framed,
-                       framed_size, d_offsets, d_lengths, n, mac, ledger_id, first_entry_id, skip_entry_check,
-                       d_status, (unsigned long long*)d_first_bad);
-    BKD_HIP(hipGetLastError());
-    return BKD_OK;
+    uint32_t *seeds = nullptr, *plen = nullptr;
+    uint64_t* poff = nullptr;
+    hipError_t e = hipMallocAsync((void**)&seeds, n * 4, st);
+    if (e == hipSuccess) e = hipMallocAsync((void**)&plen, n * 4, st);
+    if (e == hipSuccess) e = hipMallocAsync((void**)&poff, n * 8, st);
+    if (e != hipSuccess) {
+        rc = fail(BKD_ERR_NOMEM, std::string("verify scratch: ") + hipGetErrorString(e));
+    } else {
+        hipLaunchKernelGGL(bkd::verify_header_kernel, dim3(blocks), dim3(256), 0, st, btab,
+                           (const uint8_t*)d_framed, framed_size, d_offsets, d_lengths, n, mac, seeds, poff, plen,
+                           d_first_bad);
+        e = hipGetLastError();
+        if (e != hipSuccess) rc = fail(BKD_ERR_HIP, hipGetErrorString(e));
+        if (!rc)  // payload CRCs land in d_status, then verify_finish turns them into status codes
+            rc = indexed_batch(*ds, algo, (const uint8_t*)d_framed, framed_size, poff, plen, n, seeds, 0,
+                               reinterpret_cast<uint32_t*>(d_status), st);
+        if (!rc) {
+            hipLaunchKernelGGL(bkd::verify_finish_kernel, dim3(blocks), dim3(256), 0, st, (const uint8_t*)d_framed,
+                               framed_size, d_offsets, d_lengths, n, mac, ledger_id, first_entry_id, id_checks,
+                               d_status, (unsigned long long*)d_first_bad);
+            e = hipGetLastError();
+            if (e != hipSuccess) rc = fail(BKD_ERR_HIP, hipGetErrorString(e));
+        }
+    }
+    for (void* p : {(void*)seeds, (void*)plen, (void*)poff})
+        if (p) (void)hipFreeAsync(p, st);
+    return rc;
+}
+}  // namespace
+
+int bkd_digest_verify_batch(int algo, int64_t ledger_id, int64_t first_entry_id, int skip_entry_check,
+                            const void* d_framed, uint64_t framed_size, const uint64_t* d_offsets,
+                            const uint32_t* d_lengths, uint64_t n, int32_t* d_status, uint64_t* d_first_bad,
+                            void* stream) {
+    return verify_framed(algo, ledger_id, first_entry_id, skip_entry_check ? 1 : 0, d_framed, framed_size,
+                         d_offsets, d_lengths, n, d_status, d_first_bad, stream);
+}
+
+int bkd_entrylog_verify(int algo, const void* d_log, uint64_t log_size, const uint64_t* d_offsets,
+                        const uint32_t* d_lengths, uint64_t n, int32_t* d_status, uint64_t* d_first_bad,
+                        void* stream) {
+    return verify_framed(algo, 0, 0, 2, d_log, log_size, d_offsets, d_lengths, n, d_status, d_first_bad, stream);
+}
+
+int bkd_entrylog_index(const void* h_log, uint64_t log_size, uint64_t start, uint64_t* h_offsets,
+                       uint32_t* h_lengths, int64_t* h_ledger_ids, uint64_t capacity, uint64_t* h_count,
+                       uint64_t* h_end) {
+    if (!h_count || (log_size && !h_log) || (capacity && (!h_offsets || !h_lengths)))
+        return fail(BKD_ERR_INVALID_ARG, "null buffer");
+    const uint8_t* p = (const uint8_t*)h_log;
+    auto be32 = [&](uint64_t at) {
+        return (int32_t)(((uint32_t)p[at] << 24) | ((uint32_t)p[at + 1] << 16) | ((uint32_t)p[at + 2] << 8) |
+                         (uint32_t)p[at + 3]);
+    };
+    auto be64 = [&](uint64_t at) {
+        uint64_t v = 0;
+        for (int k = 0; k < 8; ++k) v = (v << 8) | p[at + k];
+        return (int64_t)v;
+    };
+    uint64_t pos = start, count = 0;
+    int rc = BKD_OK;
+    while (pos < log_size) {
+        if (log_size - pos < 12) break;  // short read of [size, ledgerId]: the scan stops
+        const int32_t entry_size = be32(pos);
+        if (entry_size <= 0) {  // padding
+            ++pos;
+            continue;
+        }
+        const int64_t ledger_id = be64(pos + 4);
+        pos += 4;
+        if (ledger_id == -1) {  // INVALID_LID: ledgers-map record, not an entry
+            pos += (uint64_t)entry_size;
+            continue;
+        }
+        if ((uint64_t)entry_size > log_size - pos) break;  // short read of the entry: the scan stops
+        if (count < capacity) {
+            h_offsets[count] = pos;
+            h_lengths[count] = (uint32_t)entry_size;
+            if (h_ledger_ids) h_ledger_ids[count] = ledger_id;
+        } else {
+            rc = fail(BKD_ERR_BOUNDS, "entry-log index capacity exceeded");
+            break;
+        }
+        ++count;
+        pos += (uint64_t)entry_size;
+    }
+    *h_count = count;
+    if (h_end) *h_end = pos;
+    return rc;
 }
 
 int bkd_fill_splitmix64(void* d_dst, uint64_t nbytes, uint64_t seed, uint64_t first_word, void* stream) {

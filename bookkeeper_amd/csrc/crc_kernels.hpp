@@ -388,10 +388,14 @@ __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __res
 }
 
 // ---- chunk descriptors of the ragged-batch plan (built by plan_kernels.hpp) ----
-// 16 bytes: s (48-bit byte offset) | len (16 bits; a chunk is at most CH + 15 < 64 KiB bytes),
-// the register folded into its first bytes, and the destination (bit 31: finalized CRC into
-// out[dst], else raw partial into partials[dst]). len == 0 marks a hole (skipped).
+// 16 bytes: s (41-bit byte offset) | pad (7 bits) | len (16 bits; a chunk is at most CH + 15 <
+// 64 KiB bytes), the register folded into its first bytes, and the destination (bit 31: finalized
+// CRC into out[dst], else raw partial into partials[dst]). len == 0 marks a hole (skipped).
+// pad > 0: the chunk [s, s+len) ends on a 128-byte line past its entry's end; its last pad bytes
+// belong to other data and are folded as zeros (the combine then multiplies by x^(-8*pad)).
 constexpr uint32_t kPlanFinal = 0x80000000u;
+constexpr int kPlanOffBits = 41;
+constexpr uint64_t kPlanMaxSize = 1ull << kPlanOffBits;
 
 struct __attribute__((aligned(16))) PlanDesc {
     uint64_t s_len;
@@ -413,12 +417,14 @@ struct ChunkGeo {
     uint32_t r0;  // register folded into the first bytes
     uint32_t dst;
     uint32_t len;
+    uint32_t pad;  // trailing bytes of the window that are not the entry's (folded as zeros)
 };
 
 template <int G>
 __device__ __forceinline__ ChunkGeo chunk_geo(const PlanDesc& d, int g) {
     ChunkGeo c;
-    c.s = (int64_t)(d.s_len & 0xFFFFFFFFFFFFull);
+    c.s = (int64_t)(d.s_len & (kPlanMaxSize - 1u));
+    c.pad = (uint32_t)(d.s_len >> kPlanOffBits) & 127u;
     c.len = (uint32_t)(d.s_len >> 48);
     const int64_t e = c.s + (int64_t)c.len;
     c.J = (uint32_t)((c.len + Geo<G>::kStep - 1) / Geo<G>::kStep);
@@ -526,6 +532,37 @@ __device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lan
     }
 #undef BKD_FOLD
 #undef BKD_FOLD0
+    if (c.pad) {
+        // the last step's block of this lane ends past the entry: its bytes >= the entry's end
+        // were folded last (XORed in after the final multiply), so XOR them out again
+        const int64_t al = a + (int64_t)(c.J - 1u) * Gm::kStep;
+        const int64_t et = s + (int64_t)c.len - (int64_t)c.pad;
+        if (al + 16 > et) {
+            u32x4 last;
+            if (rem == 0u) {
+                last = W0;
+            } else if (rem <= (uint32_t)PF) {
+                last = A[0];
+#pragma unroll
+                for (int k = 1; k < PF; ++k)
+                    if ((uint32_t)k == rem - 1u) last = A[k];
+            } else {
+                const uint32_t left = (rem - (uint32_t)PF) % (2u * PF);
+                last = A[PF - 1];
+#pragma unroll
+                for (int k = 0; k < PF; ++k) {
+                    if ((uint32_t)k + 1u == left) last = B[k];
+                    if ((uint32_t)(PF + k) + 1u == left) last = A[k];
+                }
+            }
+            const int64_t keep = et - al;
+            const u32x4 junk = keep <= 0 ? last : mask_low_bytes(last, (uint32_t)keep);
+            c0 ^= junk.x;
+            c1 ^= junk.y;
+            c2 ^= junk.z;
+            c3 ^= junk.w;
+        }
+    }
     uint32_t v;
     if constexpr (Gm::kFast) {
         v = mul_aux(lds, Gm::kX96Off, c0) ^ mul_aux(lds, Gm::kX64Off, c1) ^ mul_aux(lds, Gm::kX32Off, c2) ^ c3;
@@ -693,11 +730,13 @@ __global__ void package_digest_kernel(const uint32_t* __restrict__ digests, uint
     f[3] = (uint8_t)d;
 }
 
-// Verify step 1: CRC of the 32-byte header of each framed entry (DigestManager.java:236).
+// Verify step 1: CRC of the 32-byte header of each framed entry (DigestManager.java:236), and the
+// payload range [o + 32 + mac, o + l) that step 2 folds from that seed (empty for a short entry).
 __global__ void verify_header_kernel(const uint32_t* __restrict__ byte_table, const uint8_t* __restrict__ framed,
                                      uint64_t size, const uint64_t* __restrict__ offsets,
                                      const uint32_t* __restrict__ lengths, uint64_t n, uint32_t mac,
-                                     uint32_t* __restrict__ seeds, uint64_t* __restrict__ first_bad) {
+                                     uint32_t* __restrict__ seeds, uint64_t* __restrict__ pay_offsets,
+                                     uint32_t* __restrict__ pay_lengths, uint64_t* __restrict__ first_bad) {
     __shared__ uint32_t bt[256];
     for (int k = threadIdx.x; k < 256; k += blockDim.x) bt[k] = byte_table[k];
     __syncthreads();
@@ -707,8 +746,16 @@ __global__ void verify_header_kernel(const uint32_t* __restrict__ byte_table, co
     const uint64_t o = offsets[i];
     const uint32_t l = lengths[i];
     uint32_t s = 0;
-    if (o <= size && (uint64_t)l <= size - o && l >= 32u + mac) s = ~crc_bytes_serial(bt, 0xFFFFFFFFu, framed + o, 32);
+    uint64_t po = 0;
+    uint32_t pl = 0;
+    if (o <= size && (uint64_t)l <= size - o && l >= 32u + mac) {
+        s = ~crc_bytes_serial(bt, 0xFFFFFFFFu, framed + o, 32);
+        po = o + 32u + mac;
+        pl = l - 32u - mac;
+    }
     seeds[i] = s;
+    pay_offsets[i] = po;
+    pay_lengths[i] = pl;
 }
 
 // Verify step 3: compare digest bytes and ids, per-entry status, first failing index
@@ -741,9 +788,10 @@ __global__ void verify_finish_kernel(const uint8_t* __restrict__ framed, uint64_
             lid = (lid << 8) | f[k];
             eid = (eid << 8) | f[8 + k];
         }
+        // skip_entry_check: 0 ledger + entry ids, 1 ledger id only, 2 digest only (entry-log scrub)
         if (!hi_zero || stored != computed) st = 2;
-        else if ((int64_t)lid != ledger_id) st = 3;
-        else if (!skip_entry_check && (int64_t)eid != first_entry_id + (int64_t)i) st = 4;
+        else if (skip_entry_check < 2 && (int64_t)lid != ledger_id) st = 3;
+        else if (skip_entry_check == 0 && (int64_t)eid != first_entry_id + (int64_t)i) st = 4;
     }
     status[i] = st;
     if (st != 0) atomicMin(first_bad, (unsigned long long)i);

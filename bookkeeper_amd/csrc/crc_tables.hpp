@@ -42,6 +42,20 @@ inline uint32_t xpow(int algo, uint64_t nbits) {
     return result;
 }
 
+// Inverse of mulx: the register before one zero bit was folded in. Prefl has bit 31 (x^0) set,
+// so bit 31 of y says whether the low bit of the pre-image was 1.
+inline uint32_t divx(int algo, uint32_t y) {
+    return (y & 0x80000000u) ? (((y ^ poly(algo)) << 1) | 1u) : (y << 1);
+}
+
+// x^(-8k) mod P: undoes k zero bytes appended to a message (the ragged plan pads each entry to
+// the next 128-byte line with zeros, plan_kernels.hpp).
+inline uint32_t xpow_neg8(int algo, uint32_t k) {
+    uint32_t r = 0x80000000u;
+    for (uint32_t i = 0; i < 8u * k; ++i) r = divx(algo, r);
+    return r;
+}
+
 // Operator "multiply a 32-bit register by C" split by byte position:
 // out[t*256 + b] = (b << 8t) * C mod P, so r*C = T0[r&255] ^ T1[r>>8&255] ^ T2[r>>16&255] ^ T3[r>>24].
 inline void operator_tables(int algo, uint32_t C, uint32_t* out) {

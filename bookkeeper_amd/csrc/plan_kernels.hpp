@@ -3,20 +3,22 @@
 // Why: a G-lane group walks its work in lockstep with the other groups of its wavefront, so a
 // wave holding Zipf-sized entries runs as long as its longest entry (SURVEY.md §7 "load balance
 // for Zipf sizes"), and packed entries start and end at arbitrary bytes. The plan therefore
-//  * splits every entry [s, e) at ae = the last 128-byte-aligned device address <= e: the <= 127
-//    tail bytes [ae, e) are folded serially by plan_combine_kernel, everything before ae is cut
-//    into chunks of CH = 16*G*JC bytes whose ends are aligned (c = 0 ends at ae, c = m-1 is the
-//    head and starts at s, carrying the seed), so every 16-byte load of the main kernel is an
-//    aligned global_load_dwordx4;
+//  * pads every entry [s, e) to ae = the first 128-byte-aligned device address >= e (64 for
+//    4-lane groups, whose 64-byte step must hold the whole pad) (the pad
+//    bytes lie in e's own 128-byte line, so reading them never leaves mapped memory; the chunk
+//    kernel folds them as zeros) and cuts [s, ae) into chunks of CH = 16*G*JC bytes whose ends
+//    are aligned (c = 0 ends at ae, c = m-1 is the head and starts at s, carrying the seed), so
+//    every 16-byte load of the main kernel is an aligned global_load_dwordx4 and no 128-byte line
+//    is fetched by two chunks;
 //  * lists the chunks in descending step count (merged heads JC+1, full chunks JC, heads JC-1..1)
 //    so that neighbouring groups, which run in lockstep, have equal work;
 //  * writes one self-contained 32-byte descriptor per chunk (range, seed register, destination),
 //    which the main kernel prefetches one round ahead — no dependent index loads at chunk start;
 //  * combines multi-chunk entries as reg = sum_c partial_c * X^c, X = x^(8*CH) (Horner from the
-//    head), then folds the tail bytes: the GPU analogue of crc32c_chunk's stream merge by shift
-//    tables (crc32c_sse42.cpp:92-134).
-// Entries whose aligned part is < 16 bytes, invalid (out-of-bounds) entries, and entries that do
-// not fit the plan's capacity (only possible when entries overlap heavily) are computed serially by
+//    head), then removes the zero padding (multiply by x^(-8*pad)): the GPU analogue of
+//    crc32c_chunk's stream merge by shift tables (crc32c_sse42.cpp:92-134).
+// Entries shorter than 16 bytes, invalid (out-of-bounds) entries, and entries that do not fit the
+// plan's capacity (only possible when entries overlap heavily) are computed serially by
 // plan_combine_kernel (correct, slow path).
 //
 // Launch sequence (caller's stream, no host sync): plan_count -> plan_scan -> plan_emit ->
@@ -38,7 +40,7 @@ struct PlanGeo {
     uint32_t step;   // 16 * G bytes
     uint32_t jc;     // steps per full chunk
     uint32_t ch;     // step * jc
-    uint32_t mis;    // device address of base modulo 16
+    uint32_t mis;    // device address of base modulo 128
     uint32_t merge;  // a head chunk shorter than this (>= 16) merges into its neighbour
     uint32_t nbins;  // bins 0 .. nbins-1: ceil((ch + merge - 1) / step) + 1
 };
@@ -48,7 +50,8 @@ constexpr int kHdrTotal = 0;  // all chunks
 constexpr int kHdrSlots = 1;  // partial slots
 constexpr int kHdrWork = 2;   // descriptors to process = min(total, capacity)
 constexpr int kHdrBig = 3;    // entries whose full chunks plan_expand_big writes
-constexpr int kHdrWords = 4;
+constexpr int kHdrBase = 4;   // kHdrBase + col: first descriptor / slot of column col
+constexpr int kHdrWords = kHdrBase + kMaxJC + 2;
 
 __device__ __forceinline__ bool entry_valid(uint64_t o, uint32_t l, uint64_t size) {
     return !(o > size || (uint64_t)l > size - o);
@@ -56,7 +59,8 @@ __device__ __forceinline__ bool entry_valid(uint64_t o, uint32_t l, uint64_t siz
 
 struct EntryPlan {
     int64_t s, e, ae;
-    uint32_t m;     // chunks of the aligned part
+    uint32_t pad;   // ae - e (0 .. 127)
+    uint32_t m;     // chunks of [s, ae)
     uint32_t jh;    // head chunk steps (1 .. nbins-1)
     uint32_t full;  // chunks in the full bucket (bin JC)
     uint32_t ps;    // partial slots (0: the single chunk writes the final CRC)
@@ -72,13 +76,16 @@ __device__ __forceinline__ EntryPlan plan_entry(uint64_t o, uint32_t l, uint64_t
     p.s = (int64_t)o;
     p.e = (int64_t)(o + l);
     // chunk ends sit on 128-byte lines: a line is then never split between two chunks that run
-    // at different times (each would fetch it from HBM); the <= 127 tail bytes go to the combine
-    const uint32_t delta = (uint32_t)((pg.mis + (uint64_t)p.e) & 127u);
-    p.ae = p.e - delta;
-    if (p.ae - p.s < 16) {
+    // at different times (each would fetch it from HBM)
+    if (l < 16u) {
         p.kind = 1;
         return p;
     }
+    // pad to the next multiple of min(step, 128): the pad then lies in the entry's last 128-byte
+    // line AND in the last step of its final chunk (the chunk kernel clears it there)
+    const uint32_t al = pg.step < 128u ? pg.step : 128u;
+    p.pad = (uint32_t)((al - ((pg.mis + (uint64_t)p.e) & (al - 1u))) & (al - 1u));
+    p.ae = p.e + (int64_t)p.pad;
     const uint64_t la = (uint64_t)(p.ae - p.s);
     uint32_t m = (uint32_t)((la + pg.ch - 1) / pg.ch);
     uint64_t hl = la - (uint64_t)(m - 1u) * pg.ch;
@@ -89,7 +96,7 @@ __device__ __forceinline__ EntryPlan plan_entry(uint64_t o, uint32_t l, uint64_t
     p.m = m;
     p.jh = (uint32_t)((hl + pg.step - 1) / pg.step);
     p.full = (m - 1u) + (p.jh == pg.jc ? 1u : 0u);
-    p.ps = (m == 1u && delta == 0u) ? 0u : m;
+    p.ps = (m == 1u && p.pad == 0u) ? 0u : m;
     p.kind = 0;
     return p;
 }
@@ -100,7 +107,8 @@ __device__ __forceinline__ PlanDesc chunk_desc(const EntryPlan& p, uint32_t c, u
     const int64_t e = p.ae - (int64_t)c * pg.ch;
     const bool head = c + 1u == p.m;
     const int64_t s = head ? p.s : e - (int64_t)pg.ch;
-    d.s_len = (uint64_t)s | ((uint64_t)(e - s) << 48);
+    const uint64_t pad = c == 0u ? (uint64_t)p.pad : 0u;
+    d.s_len = (uint64_t)s | (pad << kPlanOffBits) | ((uint64_t)(e - s) << 48);
     d.r0 = head ? ~seed : 0u;
     d.dst = p.ps == 0u ? (entry | kPlanFinal) : slot + c;
     return d;
@@ -147,13 +155,24 @@ __global__ void __launch_bounds__(kPlanBlock) plan_count_kernel(const uint64_t* 
     for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) col[k] = 0u;
     __syncthreads();
     const uint64_t i = (uint64_t)blockIdx.x * kPlanBlock + threadIdx.x;
+    uint32_t full = 0u, ps = 0u;
     if (i < n) {
         const EntryPlan p = plan_entry(offsets[i], lengths[i], size, pg);
         if (p.kind == 0) {
             if (p.jh != pg.jc) atomicAdd(&col[p.jh], 1u);
-            if (p.full) atomicAdd(&col[pg.jc], p.full);
-            if (p.ps) atomicAdd(&col[slot_col(pg)], p.ps);
+            full = p.full;
+            ps = p.ps;
         }
+    }
+    // every entry adds to these two columns: one LDS atomic per wave instead of 64
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        full += (uint32_t)__shfl_xor((int)full, d);
+        ps += (uint32_t)__shfl_xor((int)ps, d);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (full) atomicAdd(&col[pg.jc], full);
+        if (ps) atomicAdd(&col[slot_col(pg)], ps);
     }
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) blk[(uint64_t)k * gridDim.x + blockIdx.x] = col[k];
@@ -202,13 +221,12 @@ __global__ void __launch_bounds__(kPlanBlock) plan_scan_kernel(const uint32_t* _
             acc += tot[j];
         }
         base[slot_col(pg)] = 0;
+        for (uint32_t c = 0; c < ncols; ++c) hdr[kHdrBase + c] = base[c];
         hdr[kHdrTotal] = acc;
         hdr[kHdrSlots] = tot[slot_col(pg)];
         hdr[kHdrWork] = (uint32_t)((uint64_t)acc < capacity ? acc : capacity);
         hdr[kHdrBig] = 0;
     }
-    __syncthreads();
-    for (uint64_t k = threadIdx.x; k < (uint64_t)nb * ncols; k += kPlanBlock) blkoff[k] += base[k / nb];
 }
 
 __global__ void __launch_bounds__(kPlanBlock) plan_emit_kernel(const uint64_t* __restrict__ offsets,
@@ -223,7 +241,8 @@ __global__ void __launch_bounds__(kPlanBlock) plan_emit_kernel(const uint64_t* _
     __shared__ uint32_t wsum[kPlanBlock / 64 + 1];
     __shared__ uint32_t cursor[kMaxJC + 2];
     const uint32_t ncols = plan_ncols(pg);
-    for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) cursor[k] = blkoff[(uint64_t)k * gridDim.x + blockIdx.x];
+    for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock)
+        cursor[k] = hdr[kHdrBase + k] + blkoff[(uint64_t)k * gridDim.x + blockIdx.x];
     __syncthreads();
     const uint64_t i = (uint64_t)blockIdx.x * kPlanBlock + threadIdx.x;
     EntryPlan p{};
@@ -278,13 +297,14 @@ __global__ void plan_expand_big_kernel(const uint64_t* __restrict__ offsets, con
     }
 }
 
-// Horner over the partial registers of each chunked entry, then its unaligned tail bytes;
-// serial fold of entries the plan did not chunk.
+// Horner over the partial registers of each chunked entry, then x^(-8*pad); serial fold of
+// entries the plan did not chunk.
 __global__ void plan_combine_kernel(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets,
                                     const uint32_t* __restrict__ lengths, const uint32_t* __restrict__ seeds,
                                     uint32_t seed_all, uint64_t size, uint64_t n, PlanGeo pg,
                                     const uint32_t* __restrict__ xtab, const uint32_t* __restrict__ x32tab,
-                                    const uint32_t* __restrict__ btab, const uint32_t* __restrict__ pslot, const uint32_t* __restrict__ partials,
+                                    const uint32_t* __restrict__ btab, const uint32_t* __restrict__ xinv,
+                                    uint32_t poly, const uint32_t* __restrict__ pslot, const uint32_t* __restrict__ partials,
                                     uint32_t* __restrict__ out, uint32_t* __restrict__ err) {
     __shared__ uint32_t X[1024];
     __shared__ uint32_t W[1024];
@@ -319,29 +339,21 @@ __global__ void plan_combine_kernel(const uint8_t* __restrict__ base, const uint
         return;
     }
     const EntryPlan p = plan_entry(o, l, size, pg);
-    const uint32_t nq = (uint32_t)(p.e - p.ae);
     uint32_t reg = partials[slot + p.m - 1u];
     for (int c = (int)p.m - 2; c >= 0; --c) {
         reg = X[reg & 0xffu] ^ X[256 + ((reg >> 8) & 0xffu)] ^ X[512 + ((reg >> 16) & 0xffu)] ^ X[768 + (reg >> 24)];
         reg ^= partials[slot + (uint32_t)c];
     }
-    // the tail [ae, e) lies in the 128-byte line at ae: 16-byte vector loads, never past that line;
-    // whole dwords advance the register by x^32 (4 independent lookups), the last 0-3 bytes by x^8
-    const u32x4* tq = reinterpret_cast<const u32x4*>(base + p.ae);
-    for (uint32_t b0 = 0; b0 < nq; b0 += 16) {
-        const u32x4 t = tq[b0 >> 4];
-        const uint32_t nb = nq - b0 < 16u ? nq - b0 : 16u;
-        const uint32_t nw = nb >> 2;
+    // undo the zero padding: reg * x^(-8*pad), a bitwise product (no table dependency chain)
+    if (p.pad) {
+        const uint32_t k = xinv[p.pad];
+        uint32_t prod = 0u, cur = reg;
 #pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-            const uint32_t w = k == 0 ? t.x : k == 1 ? t.y : k == 2 ? t.z : t.w;
-            if (k < nw) {
-                const uint32_t r = reg ^ w;
-                reg = W[r & 0xffu] ^ W[256 + ((r >> 8) & 0xffu)] ^ W[512 + ((r >> 16) & 0xffu)] ^ W[768 + (r >> 24)];
-            } else if (k == nw) {
-                for (uint32_t j = 0; j < (nb & 3u); ++j) reg = B[(reg ^ (w >> (8 * j))) & 0xffu] ^ (reg >> 8);
-            }
+        for (int b = 31; b >= 0; --b) {
+            prod ^= ((k >> b) & 1u) ? cur : 0u;
+            cur = (cur >> 1) ^ ((cur & 1u) ? poly : 0u);
         }
+        reg = prod;
     }
     out[i] = ~reg;
 }

@@ -132,6 +132,31 @@ int bkd_digest_verify_batch(int algo, int64_t ledger_id, int64_t first_entry_id,
                             const uint32_t* d_lengths, uint64_t n, int32_t* d_status, uint64_t* d_first_bad,
                             void* stream);
 
+/* ---- bookie-side entry-log scrub (§8f row 4) ------------------------------------------
+ * An entry log is a 1024-byte file header (LOGFILE_HEADER_SIZE, DefaultEntryLogger.java:256)
+ * followed by records [int32 BE size][entry bytes], an entry starting with its BE ledger id.
+ *
+ * Index: walks the records of a HOST buffer from byte `start` exactly like
+ * DefaultEntryLogger.scanEntryLog ($BK/bookie/DefaultEntryLogger.java:995-1060): size <= 0 is
+ * padding (advance one byte), ledger id -1 (INVALID_LID) is a ledgers-map record (skipped), a
+ * short read of the 12-byte [size, ledgerId] header or of the entry ends the scan. Writes each
+ * entry's offset (first byte after the size field), length and ledger id; *h_end = the position
+ * where the walk stopped. BKD_ERR_BOUNDS when more than `capacity` entries are found.
+ * Host-only control logic: it reads 12 bytes per record and computes no digest. */
+int bkd_entrylog_index(const void* h_log, uint64_t log_size, uint64_t start, uint64_t* h_offsets,
+                       uint32_t* h_lengths, int64_t* h_ledger_ids, uint64_t capacity, uint64_t* h_count,
+                       uint64_t* h_end);
+
+/* Verify: the digest of every indexed entry of a DEVICE-resident log, as
+ * DigestManager.verifyDigest would (DigestManager.java:226-283: CRC of [0,32) || [32+mac, len)
+ * against the stored digest at 32) without ledger/entry id checks (the ledger id comes from the
+ * entry itself). Status codes as bkd_digest_verify_batch (0 ok, 1 too short, 2 digest mismatch);
+ * *d_first_bad = first failing index or n. One digest type per call (the ledger's, from its
+ * metadata). Asynchronous on `stream`; ragged batches go through the chunked plan. */
+int bkd_entrylog_verify(int algo, const void* d_log, uint64_t log_size, const uint64_t* d_offsets,
+                        const uint32_t* d_lengths, uint64_t n, int32_t* d_status, uint64_t* d_first_bad,
+                        void* stream);
+
 /* ---- synthetic input + test helpers --------------------------------------------------- */
 
 /* Fills nbytes of device memory with the little-endian splitmix64 stream

@@ -84,6 +84,9 @@ def lib():
                                           ctypes.c_int]
         L.oracle_fill_splitmix64.restype = None
         L.oracle_fill_splitmix64.argtypes = [_u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
+        L.oracle_entrylog_scan.restype = ctypes.c_uint64
+        L.oracle_entrylog_scan.argtypes = [_u8p, ctypes.c_uint64, ctypes.c_uint64, _u64p, _u32p,
+                                           ctypes.POINTER(ctypes.c_int64), ctypes.c_uint64, _u64p]
         L.oracle_table.restype = None
         L.oracle_table.argtypes = [ctypes.c_int, _u32p]
         _lib = L
@@ -198,3 +201,16 @@ def fill_splitmix64(nbytes: int, seed: int, first_word: int = 0) -> np.ndarray:
     out = np.zeros(nbytes, dtype=np.uint8)
     lib().oracle_fill_splitmix64(_ptr(out, _u8p), nbytes, seed, first_word)
     return out
+
+
+def entrylog_scan(log, start: int = 1024):
+    """DefaultEntryLogger.scanEntryLog restated: (offsets u64, lengths u32, ledger ids i64, end)."""
+    a = _as_u8(log)
+    cap = max(1, a.size // 16)
+    offs = np.zeros(cap, dtype=np.uint64)
+    lens = np.zeros(cap, dtype=np.uint32)
+    lids = np.zeros(cap, dtype=np.int64)
+    end = np.zeros(1, dtype=np.uint64)
+    n = int(lib().oracle_entrylog_scan(_ptr(a, _u8p), a.size, start, _ptr(offs, _u64p), _ptr(lens, _u32p),
+                                       lids.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), cap, _ptr(end, _u64p)))
+    return offs[:n], lens[:n], lids[:n], int(end[0])

@@ -194,3 +194,30 @@ void oracle_fill_splitmix64(uint8_t* dst, uint64_t nbytes, uint64_t seed, uint64
         memcpy(dst + 8 * nw, &v, rem);
     }
 }
+
+/* ---- Entry-log record walk (DefaultEntryLogger.scanEntryLog, DefaultEntryLogger.java:995-1060). ----
+ * From `start` (LOGFILE_HEADER_SIZE = 1024, :256): read [int32 BE size][int64 BE ledgerId]
+ * (a short read of these 12 bytes ends the scan, :1020-1023); size <= 0 is padding -> pos++
+ * (:1027-1031); ledgerId == INVALID_LID (-1) -> skip the record (:1037-1041); a short read of the
+ * entry ends the scan (:1046-1054); else the entry is [pos+4, pos+4+size). Returns the count,
+ * writes at most `cap` entries and the final position to *end. */
+uint64_t oracle_entrylog_scan(const uint8_t* log, uint64_t size, uint64_t start, uint64_t* offs,
+                              uint32_t* lens, int64_t* lids, uint64_t cap, uint64_t* end) {
+    uint64_t pos = start, n = 0;
+    while (pos < size) {
+        if (size - pos < 12) break;
+        int32_t esz = (int32_t)(((uint32_t)log[pos] << 24) | ((uint32_t)log[pos + 1] << 16) |
+                                ((uint32_t)log[pos + 2] << 8) | (uint32_t)log[pos + 3]);
+        if (esz <= 0) { pos++; continue; }
+        uint64_t lid = 0;
+        for (int i = 0; i < 8; ++i) lid = (lid << 8) | log[pos + 4 + i];
+        pos += 4;
+        if ((int64_t)lid == -1) { pos += (uint64_t)esz; continue; }
+        if ((uint64_t)esz > size - pos) break;
+        if (n < cap) { offs[n] = pos; lens[n] = (uint32_t)esz; lids[n] = (int64_t)lid; }
+        n++;
+        pos += (uint64_t)esz;
+    }
+    if (end) *end = pos;
+    return n;
+}

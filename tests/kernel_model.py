@@ -86,23 +86,27 @@ class KernelModel:
 def plan_model(tables_by_lanes, algo_xpow8n, gf_mul, data: bytes, seed: int, lanes: int = 8, jc: int = 32,
                mis: int = 0) -> int:  # mis: entry start address modulo 128
     """Models the ragged-batch plan (plan_kernels.hpp) for one entry starting at a device address
-    congruent to `mis` (mod 16): the aligned part [0, ae) is cut into chunks of CH = 16*lanes*jc bytes
-    ending at aligned addresses (head chunk carries the seed; a head < 16 B merges into its
-    neighbour), each chunk folded by the kernel decomposition (aligned straddle masking), partial
-    registers combined by Horner with X = x^(8*CH), then the tail bytes [ae, e) folded serially."""
+    congruent to `mis` (mod 128): the entry is padded with zeros to ae = the next 128-byte-aligned
+    address (the kernel folds the foreign bytes there and XORs them out again, which equals folding
+    zeros), [0, ae) is cut into chunks of CH = 16*lanes*jc bytes ending at aligned addresses (head
+    chunk carries the seed; a head < 16 B merges into its neighbour), each chunk folded by the kernel
+    decomposition, partial registers combined by Horner with X = x^(8*CH), then multiplied by
+    x^(-8*pad). Entries shorter than 16 bytes are folded serially."""
     ch, step = 16 * lanes * jc, 16 * lanes
     km = KernelModel(tables_by_lanes, lanes)
     n = len(data)
     byte = km.byte
+    poly = int(byte[0x80])  # T[0x80] = P for a reflected CRC
 
-    def serial(reg, bs):
-        for b in bs:
+    if n < 16:
+        reg = (~seed) & 0xFFFFFFFF
+        for b in data:
             reg = int(byte[(reg ^ b) & 0xFF]) ^ (reg >> 8)
-        return reg
-
-    ae = n - ((mis + n) & 127)
-    if ae < 16:
-        return (~serial((~seed) & 0xFFFFFFFF, data)) & 0xFFFFFFFF
+        return (~reg) & 0xFFFFFFFF
+    al = min(step, 128)  # the pad must fit the final chunk's last step
+    pad = (al - ((mis + n) & (al - 1))) & (al - 1)
+    padded = bytes(data) + bytes(pad)
+    ae = n + pad
     m = (ae + ch - 1) // ch
     hl = ae - (m - 1) * ch
     if hl < 16 and m > 1:
@@ -112,11 +116,14 @@ def plan_model(tables_by_lanes, algo_xpow8n, gf_mul, data: bytes, seed: int, lan
         e = ae - c * ch
         cs = 0 if c == m - 1 else e - ch
         r0 = (~seed) & 0xFFFFFFFF if c == m - 1 else 0
-        # raw register of data[cs:e] with r0 folded in == ~KernelModel.crc(chunk, ~r0)
-        parts.append((~km.crc(data[cs:e], (~r0) & 0xFFFFFFFF)) & 0xFFFFFFFF)
+        # raw register of padded[cs:e] with r0 folded in == ~KernelModel.crc(chunk, ~r0)
+        parts.append((~km.crc(padded[cs:e], (~r0) & 0xFFFFFFFF)) & 0xFFFFFFFF)
         assert (e - cs) <= ch + 15 and (e - cs + step - 1) // step <= jc + 1
     X = algo_xpow8n(ch)
     reg = parts[m - 1]
     for c in range(m - 2, -1, -1):
         reg = gf_mul(reg, X) ^ parts[c]
-    return (~serial(reg, data[ae:])) & 0xFFFFFFFF
+    inv = 0x80000000  # x^(-8*pad): divide by x, 8*pad times
+    for _ in range(8 * pad):
+        inv = (((inv ^ poly) << 1) | 1) & 0xFFFFFFFF if inv & 0x80000000 else (inv << 1) & 0xFFFFFFFF
+    return (~gf_mul(reg, inv)) & 0xFFFFFFFF

@@ -397,3 +397,31 @@ def test_host_batch_pipelined_segments(gpu, pinned):
     perm = rng.permutation(lens.size)[:200]
     got = ck.crc_batch_host(ck.CRC32, host, offs[perm], lens[perm])
     assert (got == oracle.batch(1, host, offs[perm], lens[perm])).all()
+
+
+@pytest.mark.parametrize("geom", [(4, 16, 16), (8, 32, 16), (16, 8, 16), (32, 4, 300)])
+@pytest.mark.parametrize("shift", [0, 5, 100])
+def test_plan_length_sweep_packed(gpu, geom, shift):
+    """Every entry length 0..2599 (plus multi-chunk lengths), packed with gaps and never overlapping,
+    so no entry falls back to the serial path: each goes through chunking, padding to the next
+    line and the x^(-8*pad) combine. Base misaligned by `shift` bytes."""
+    import torch
+    ck.set_plan_mode(2)
+    ck.set_plan_geometry(*geom)
+    try:
+        lens = np.concatenate([np.arange(0, 2600), np.arange(2600, 70000, 997)]).astype(np.int64)
+        gaps = (np.arange(len(lens)) * 37) % 91
+        offs = np.concatenate([[0], np.cumsum(lens + gaps)[:-1]]).astype(np.int64) + 3
+        size = int(offs[-1] + lens[-1] + 64)
+        data = oracle.fill_splitmix64(size + shift, 11)
+        big = _dev_bytes(torch, data, gpu)
+        base, host = big[shift:], data[shift:]
+        seeds = (np.arange(len(lens), dtype=np.uint64) * 2654435761 % 2**32).astype(np.uint32)
+        for algo in (ck.CRC32C, ck.CRC32):
+            got = ck.crc_batch(algo, base, torch.from_numpy(offs).to(gpu), torch.from_numpy(lens.astype(np.int32)).to(gpu),
+                               seeds=torch.from_numpy(seeds.view(np.int32)).to(gpu), sync_check=True)
+            want = oracle.batch(algo, host, offs, lens, seeds=seeds)
+            bad = np.nonzero(got.cpu().numpy().view(np.uint32) != want)[0]
+            assert len(bad) == 0, (algo, lens[bad[:10]].tolist())
+    finally:
+        ck.set_plan_geometry()
