@@ -111,9 +111,46 @@ def cpu_baseline(host_sample: np.ndarray, entry_len: int, algo: int = 0, budget_
     t = run(cores, reps)
     value = host_sample.size * reps / t / GIB
     return {"value": round(value, 3), "unit": "GiB/s", "cores": cores, "kind": kind,
-            "single_core_value": round(one_core, 3),
+            "single_core_value": round(one_core, 3), "cpu_model": _cpu_model(),
             "sample": f"{n} x {entry_len} B entries of the same splitmix64 input ({host_sample.size / GIB:.3f} GiB), "
                       f"{reps} passes over {cores} std::threads, one call per entry; {label}"}, out
+
+
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:  # pragma: no cover
+        pass
+    return "unknown"
+
+
+def bucket_rates(ck, torch, algo, base, offs, lens, stream, steps: int) -> dict:
+    """Config 3's size buckets measured on their own: the entries < 1 KiB and the
+    entries >= 16 KiB of the same packed buffer, each as one indexed batch."""
+    res = {}
+    dev = base.device
+    for name, mask in (("lt_1KiB", lens < 1024), ("ge_16KiB", lens >= 16384)):
+        idx = np.nonzero(mask)[0]
+        if idx.size == 0:
+            continue
+        d_off = torch.from_numpy(offs[idx]).to(dev)
+        d_len = torch.from_numpy(lens[idx].astype(np.int32)).to(dev)
+        out = torch.empty(idx.size, dtype=torch.int32, device=dev)
+        ck.crc_batch(algo, base, d_off, d_len, out=out, stream=stream)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(steps):
+            ck.crc_batch(algo, base, d_off, d_len, out=out, stream=stream)
+        b.record(stream)
+        torch.cuda.synchronize()
+        t = a.elapsed_time(b) / 1e3 / steps
+        nbytes = int(lens[idx].sum())
+        res[name] = {"entries": int(idx.size), "bytes": nbytes, "ms": round(t * 1e3, 4),
+                     "GiB_s": round(nbytes / t / GIB, 1), "entries_per_s": round(idx.size / t, 0)}
+    return res
 
 
 def host_bench(args, ck, torch, rank) -> None:
@@ -278,6 +315,8 @@ def main() -> None:
                      "kernel": kernel_name, "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
                      "algorithmic_bytes_per_launch": algo_bytes},
     }
+    if args.config == "zipf" and world == 1:
+        result["buckets"] = bucket_rates(ck, torch, algo, base, offs, lens, stream, max(3, args.steps))
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in ("uniform4k", "shard8m"):
         # cpu_baseline leg: the reference timed on the host cores over a bounded sample; its
         # digests for that sample double as a parity spot check of the GPU output.

@@ -142,13 +142,15 @@ int ensure_current(DeviceState** out) {
     return BKD_OK;
 }
 
-int auto_lanes(uint64_t mean_len) {
+// Lanes per entry group for the direct kernel, from the size sweep (profiles/r01_size_sweep.log):
+// 4 lanes below 512 B, 8 up to 32 KiB, 32 above; then more lanes while the batch would not give
+// every lane slot of the chip (CUs x 1024) one group lane, so a few huge entries still fill it.
+int auto_lanes(uint64_t mean_len, uint64_t n = UINT64_MAX, int cus = 256) {
     const int forced = g_forced_lanes.load();
     if (forced) return forced;
-    if (mean_len < 1024) return 4;
-    if (mean_len < 16384) return 8;
-    if (mean_len < 65536) return 16;
-    return 32;
+    int g = mean_len < 512 ? 4 : (mean_len < 32768 ? 8 : 32);
+    while (g < 64 && n < UINT64_MAX / 64 && n * (uint64_t)g < (uint64_t)cus * 1024u) g *= 2;
+    return g;
 }
 
 // Loads in flight per lane (register double buffer depth) and load cache policy; build-time
@@ -241,9 +243,8 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
         rc = fail(BKD_ERR_NOMEM, std::string("plan scratch: ") + hipGetErrorString(e));
     } else {
         hipLaunchKernelGGL(bkd::plan_count_kernel, dim3(nb), dim3(bkd::kPlanBlock), 0, st, offsets, lengths, size, n,
-                           pg, blk);
-        hipLaunchKernelGGL(bkd::plan_scan_kernel, dim3(1), dim3(bkd::kPlanBlock), 0, st, blk, nb, pg, capacity,
-                           blkoff, hdr);
+                           pg, blk, hdr);
+        hipLaunchKernelGGL(bkd::plan_scan_kernel, dim3(ncols), dim3(64), 0, st, blk, nb, blkoff, hdr);
         hipLaunchKernelGGL(bkd::plan_emit_kernel, dim3(nb), dim3(bkd::kPlanBlock), 0, st, offsets, lengths, seeds,
                            seed_all, size, n, pg, capacity, blkoff, pslot, run_start, big, hdr, descs);
         hipLaunchKernelGGL(bkd::plan_expand_big_kernel, dim3((unsigned)ds.cus), dim3(256), 0, st, offsets, lengths,
@@ -277,7 +278,7 @@ int indexed_batch(DeviceState& ds, int algo, const uint8_t* base, uint64_t size,
     const bool direct = mode == 1 || (mode == 0 && size <= kDirectMaxBytes) || size >= bkd::kPlanMaxSize;
     if (!direct) return launch_plan(ds, algo, base, size, offsets, lengths, n, seeds, seed_all, out, st);
     bkd::IndexedSrc src{n, offsets, lengths, seeds, seed_all, size, out};
-    return dispatch_lanes(ds, auto_lanes(n ? size / n : 0), algo, base, src, n, st);
+    return dispatch_lanes(ds, auto_lanes(n ? size / n : 0, n, ds.cus), algo, base, src, n, st);
 }
 
 bool valid_algo(int algo) { return algo == BKD_CRC32C || algo == BKD_CRC32; }
@@ -524,7 +525,8 @@ int bkd_crc_batch_uniform(int algo, const void* d_base, uint64_t stride, uint32_
     int rc = ensure_current(&ds);
     if (rc) return rc;
     bkd::UniformSrc src{n, stride, entry_len, d_seeds, seed_all, d_out};
-    return dispatch_lanes(*ds, auto_lanes(entry_len), algo, (const uint8_t*)d_base, src, n, (hipStream_t)stream);
+    return dispatch_lanes(*ds, auto_lanes(entry_len, n, ds->cus), algo, (const uint8_t*)d_base, src, n,
+                         (hipStream_t)stream);
 }
 
 int bkd_crc_batch(int algo, const void* d_base, uint64_t base_size, const uint64_t* d_offsets,
@@ -633,7 +635,7 @@ int bkd_digest_package_batch(int algo, int64_t ledger_id, const int64_t* d_entry
     int rc = ensure_current(&ds);
     if (rc) return rc;
     hipStream_t st = (hipStream_t)stream;
-    const int lanes = auto_lanes(payload_size / n);
+    const int lanes = auto_lanes(payload_size / n, n, ds->cus);
     const uint32_t* tab = ds->tables[algo][lane_index(lanes)];
     const uint32_t* btab = tab + bkd::gf2::byte_table_offset(lanes);
     const unsigned blocks = (unsigned)((n + 255) / 256);

@@ -50,7 +50,7 @@ constexpr int kHdrTotal = 0;  // all chunks
 constexpr int kHdrSlots = 1;  // partial slots
 constexpr int kHdrWork = 2;   // descriptors to process = min(total, capacity)
 constexpr int kHdrBig = 3;    // entries whose full chunks plan_expand_big writes
-constexpr int kHdrBase = 4;   // kHdrBase + col: first descriptor / slot of column col
+constexpr int kHdrBase = 4;   // kHdrBase + col: total of column col (plan_scan)
 constexpr int kHdrWords = kHdrBase + kMaxJC + 2;
 
 __device__ __forceinline__ bool entry_valid(uint64_t o, uint32_t l, uint64_t size) {
@@ -149,8 +149,10 @@ __device__ __forceinline__ uint32_t slot_col(const PlanGeo& pg) { return pg.nbin
 
 __global__ void __launch_bounds__(kPlanBlock) plan_count_kernel(const uint64_t* __restrict__ offsets,
                                                                 const uint32_t* __restrict__ lengths, uint64_t size,
-                                                                uint64_t n, PlanGeo pg, uint32_t* __restrict__ blk) {
+                                                                uint64_t n, PlanGeo pg, uint32_t* __restrict__ blk,
+                                                                uint32_t* __restrict__ hdr) {
     __shared__ uint32_t col[kMaxJC + 2];
+    if (blockIdx.x == 0 && threadIdx.x == 0) hdr[kHdrBig] = 0;
     const uint32_t ncols = plan_ncols(pg);
     for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) col[k] = 0u;
     __syncthreads();
@@ -178,55 +180,37 @@ __global__ void __launch_bounds__(kPlanBlock) plan_count_kernel(const uint64_t* 
     for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) blk[(uint64_t)k * gridDim.x + blockIdx.x] = col[k];
 }
 
-// One block: each wave scans whole columns across blocks (column-major, coalesced; 64 rows per
-// pass, carry in a register), then bins are placed in descending step count.
-__global__ void __launch_bounds__(kPlanBlock) plan_scan_kernel(const uint32_t* __restrict__ blk, uint32_t nb, PlanGeo pg,
-                                                               uint64_t capacity, uint32_t* __restrict__ blkoff,
-                                                               uint32_t* __restrict__ hdr) {
-    __shared__ uint32_t tot[kMaxJC + 2];
-    __shared__ uint32_t base[kMaxJC + 2];
-    const uint32_t ncols = plan_ncols(pg);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (uint32_t c = (uint32_t)wave; c < ncols; c += kPlanBlock / 64) {
-        const uint32_t* col = blk + (uint64_t)c * nb;
-        uint32_t* dst = blkoff + (uint64_t)c * nb;
-        uint32_t carry = 0;
-        for (uint32_t b1 = 0; b1 < nb; b1 += 64 * 16) {
-            uint32_t v[16];  // 16 rows per lane in flight before the dependent scans
+// One 64-lane block per column: exclusive scan of the column's per-block counts across blocks
+// (coalesced, 16 rows per lane in flight, carry in a register); the column total goes to
+// hdr[kHdrBase + col]. plan_emit places the bins (descending step count) from those totals.
+__global__ void __launch_bounds__(64) plan_scan_kernel(const uint32_t* __restrict__ blk, uint32_t nb,
+                                                       uint32_t* __restrict__ blkoff, uint32_t* __restrict__ hdr) {
+    const uint32_t c = blockIdx.x;
+    const int lane = threadIdx.x;
+    const uint32_t* col = blk + (uint64_t)c * nb;
+    uint32_t* dst = blkoff + (uint64_t)c * nb;
+    uint32_t carry = 0;
+    for (uint32_t b1 = 0; b1 < nb; b1 += 64 * 16) {
+        uint32_t v[16];
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const uint32_t b = b1 + (uint32_t)r * 64 + (uint32_t)lane;
-                v[r] = b < nb ? col[b] : 0u;
-            }
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const uint32_t b = b1 + (uint32_t)r * 64 + (uint32_t)lane;
-                uint32_t x = v[r];
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const uint32_t y = (uint32_t)__shfl_up((int)x, d);
-                    if (lane >= d) x += y;
-                }
-                if (b < nb) dst[b] = carry + x - v[r];
-                carry += (uint32_t)__shfl((int)x, 63);
-            }
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t b = b1 + (uint32_t)r * 64 + (uint32_t)lane;
+            v[r] = b < nb ? col[b] : 0u;
         }
-        if (lane == 0) tot[c] = carry;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t acc = 0;
-        for (int j = (int)pg.nbins - 1; j >= 0; --j) {  // descending step count (bin JC = full chunks)
-            base[j] = acc;
-            acc += tot[j];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t b = b1 + (uint32_t)r * 64 + (uint32_t)lane;
+            uint32_t x = v[r];
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)x, d);
+                if (lane >= d) x += y;
+            }
+            if (b < nb) dst[b] = carry + x - v[r];
+            carry += (uint32_t)__shfl((int)x, 63);
         }
-        base[slot_col(pg)] = 0;
-        for (uint32_t c = 0; c < ncols; ++c) hdr[kHdrBase + c] = base[c];
-        hdr[kHdrTotal] = acc;
-        hdr[kHdrSlots] = tot[slot_col(pg)];
-        hdr[kHdrWork] = (uint32_t)((uint64_t)acc < capacity ? acc : capacity);
-        hdr[kHdrBig] = 0;
     }
+    if (lane == 0) hdr[kHdrBase + c] = carry;
 }
 
 __global__ void __launch_bounds__(kPlanBlock) plan_emit_kernel(const uint64_t* __restrict__ offsets,
@@ -241,8 +225,25 @@ __global__ void __launch_bounds__(kPlanBlock) plan_emit_kernel(const uint64_t* _
     __shared__ uint32_t wsum[kPlanBlock / 64 + 1];
     __shared__ uint32_t cursor[kMaxJC + 2];
     const uint32_t ncols = plan_ncols(pg);
-    for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock)
-        cursor[k] = hdr[kHdrBase + k] + blkoff[(uint64_t)k * gridDim.x + blockIdx.x];
+    for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) cursor[k] = hdr[kHdrBase + k];
+    __syncthreads();
+    if (threadIdx.x == 0) {  // column totals -> first position of each bin, descending step count
+        uint32_t acc = 0;
+        for (int j = (int)pg.nbins - 1; j >= 0; --j) {
+            const uint32_t t = cursor[j];
+            cursor[j] = acc;
+            acc += t;
+        }
+        const uint32_t slots = cursor[slot_col(pg)];
+        cursor[slot_col(pg)] = 0;
+        if (blockIdx.x == 0) {
+            hdr[kHdrTotal] = acc;
+            hdr[kHdrSlots] = slots;
+            hdr[kHdrWork] = (uint32_t)((uint64_t)acc < capacity ? acc : capacity);
+        }
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) cursor[k] += blkoff[(uint64_t)k * gridDim.x + blockIdx.x];
     __syncthreads();
     const uint64_t i = (uint64_t)blockIdx.x * kPlanBlock + threadIdx.x;
     EntryPlan p{};
