@@ -186,8 +186,8 @@ def host_bench(args, ck, torch, rank) -> None:
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default="uniform4k", choices=["uniform4k", "shard8m", "zipf", "indexed4k", "host4k"])
     ap.add_argument("--algo", default="crc32c", choices=["crc32c", "crc32"])
     ap.add_argument("--entries", type=int, default=0, help="entries per GPU (default by config)")
@@ -196,6 +196,7 @@ def main() -> None:
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--zipf-align", type=int, default=1, help="diagnostic: align Zipf entries")
     ap.add_argument("--plan-mode", type=int, default=0, help="0 auto, 1 direct, 2 chunked plan")
+    ap.add_argument("--no-buckets", action="store_true", help="zipf: skip the per-bucket timings")
     ap.add_argument("--pageable", action="store_true", help="host4k: pageable instead of pinned host buffer")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL) on a real node; gloo only to rehearse several ranks on one GPU")
@@ -272,21 +273,22 @@ def main() -> None:
         step()
     torch.cuda.synchronize()
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # HIP events on the launch stream bracket the K back-to-back launches (no event packets between
+    # launches); the average launch duration is their span / K
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        ev[k][0].record(stream)
+    ev0.record(stream)
+    for _ in range(args.steps):
         step()
-        ev[k][1].record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = [a.elapsed_time(b) for a, b in ev]
-    avg_kernel_s = float(np.mean(kernel_ms)) / 1e3
+    avg_kernel_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
 
     elapsed_max = max_over_ranks(elapsed, dev if args.dist_backend == "nccl" else None)
 
@@ -315,7 +317,7 @@ def main() -> None:
                      "kernel": kernel_name, "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
                      "algorithmic_bytes_per_launch": algo_bytes},
     }
-    if args.config == "zipf" and world == 1:
+    if args.config == "zipf" and world == 1 and not args.no_buckets:
         result["buckets"] = bucket_rates(ck, torch, algo, base, offs, lens, stream, max(3, args.steps))
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in ("uniform4k", "shard8m"):
         # cpu_baseline leg: the reference timed on the host cores over a bounded sample; its

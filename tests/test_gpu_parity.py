@@ -425,3 +425,31 @@ def test_plan_length_sweep_packed(gpu, geom, shift):
             assert len(bad) == 0, (algo, lens[bad[:10]].tolist())
     finally:
         ck.set_plan_geometry()
+
+
+def test_zipf_full_size_plan_equals_direct(gpu):
+    """BASELINE config 3 at full size (1M Zipf entries, 6.8 GB): the chunked plan and the
+    one-entry-per-group kernel are independent decompositions and must agree on every entry; a
+    random sample of entries is also checked against the oracle."""
+    import torch
+    from bench import zipf_index
+    offs, lens = zipf_index(1 << 20)
+    total = int(offs[-1] + lens[-1])
+    base = torch.empty(total, dtype=torch.uint8, device=gpu)
+    ck.fill_splitmix64(base, 42)
+    d_off = torch.from_numpy(offs).to(gpu)
+    d_len = torch.from_numpy(lens.astype(np.int32)).to(gpu)
+    rng = np.random.default_rng(3)
+    pick = np.sort(rng.choice(offs.size, 2000, replace=False))
+    for algo in (ck.CRC32C, ck.CRC32):
+        ck.set_plan_mode(2)
+        plan = ck.crc_batch(algo, base, d_off, d_len, sync_check=True).cpu().numpy().view(np.uint32)
+        ck.set_plan_mode(1)
+        direct = ck.crc_batch(algo, base, d_off, d_len, sync_check=True).cpu().numpy().view(np.uint32)
+        assert (plan == direct).all()
+        parts = [base[int(offs[i]):int(offs[i] + lens[i])].cpu().numpy() for i in pick]
+        host = np.concatenate(parts)
+        sub_offs = np.concatenate([[0], np.cumsum(lens[pick])[:-1]]).astype(np.int64)
+        want = oracle.batch(algo, host, sub_offs, lens[pick])
+        assert (plan[pick] == want).all()
+    ck.set_plan_mode(0)

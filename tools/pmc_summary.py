@@ -1,40 +1,68 @@
-"""Summarise rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) for the CRC kernel into
-profiles/pmc_<config>.json. gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports
-half the bytes of a wide coalesced streaming read, so read bytes = 2 * FETCH_SIZE * 1024;
-WRITE_SIZE is exact for 16 B/lane streaming stores (our 4 B/lane digest stores are uncalibrated,
-and are 0.1 % of the traffic)."""
+"""Summarise rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) into profiles/pmc_<config>.json.
+
+gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports half the bytes of a wide
+coalesced streaming read, so read bytes = 2 * FETCH_SIZE * 1024 for the streaming CRC kernels
+(crc_groups_kernel, crc_plan_chunks_kernel); WRITE_SIZE is exact for 16 B/lane streaming stores
+(the 4 B/lane digest stores are uncalibrated and a small share of the traffic). The plan's small
+index/descriptor kernels (plan_*) are reported separately, raw (no correction: their accesses are
+not wide streaming reads).
+
+usage: pmc_summary.py FETCH_DIR WRITE_DIR CONFIG ALGO_BYTES_PER_LAUNCH [MAIN_KERNEL]"""
 import csv, glob, json, os, sys
 from collections import defaultdict
 
 
 def load(pattern):
-    vals = defaultdict(list)
+    """kernel short name -> counter -> list of per-dispatch values (summed over the dispatch's rows)."""
+    per = defaultdict(lambda: defaultdict(float))
+    names = {}
     for path in glob.glob(pattern, recursive=True):
         for row in csv.DictReader(open(path)):
             name = row.get("Kernel_Name", "")
-            if "crc_groups_kernel" not in name:
+            if "bkd::" not in name or "fill_splitmix64" in name:
                 continue
-            vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
-    return vals
+            key = (path, row.get("Dispatch_Id", row.get("Correlation_Id", "")))
+            per[key][row["Counter_Name"]] += float(row["Counter_Value"])
+            names[key] = name.split("(")[0].replace("void ", "").split("<")[0]
+    out = defaultdict(lambda: defaultdict(list))
+    for key, ctrs in per.items():
+        for c, v in ctrs.items():
+            out[names[key]][c].append(v)
+    return out
 
 
-def main(fetch_dir, write_dir, config, algo_bytes):
+def median(v):
+    v = sorted(v)
+    return v[len(v) // 2] if v else 0.0
+
+
+def main(fetch_dir, write_dir, config, algo_bytes, main_kernel="bkd::crc_groups_kernel"):
     f = load(os.path.join(fetch_dir, "**", "*counter_collection.csv"))
     w = load(os.path.join(write_dir, "**", "*counter_collection.csv"))
-    fetch_kb = sorted(f["FETCH_SIZE"])[len(f["FETCH_SIZE"]) // 2]
-    write_kb = sorted(w["WRITE_SIZE"])[len(w["WRITE_SIZE"]) // 2]
+    fetch_kb = median(f[main_kernel]["FETCH_SIZE"])
+    write_kb = median(w[main_kernel]["WRITE_SIZE"])
     read_b = 2 * fetch_kb * 1024
     write_b = write_kb * 1024
-    out = {"config": config, "kernel": "crc_groups_kernel", "dispatches": len(f["FETCH_SIZE"]),
+    aux = {}
+    for k in sorted(set(f) | set(w)):
+        if k == main_kernel:
+            continue
+        aux[k] = {"FETCH_SIZE_kB_median_raw": median(f[k]["FETCH_SIZE"]),
+                  "WRITE_SIZE_kB_median": median(w[k]["WRITE_SIZE"])}
+    aux_b = sum((a["FETCH_SIZE_kB_median_raw"] + a["WRITE_SIZE_kB_median"]) * 1024 for a in aux.values())
+    out = {"config": config, "kernel": main_kernel, "dispatches": len(f[main_kernel]["FETCH_SIZE"]),
            "FETCH_SIZE_kB_median": fetch_kb, "WRITE_SIZE_kB_median": write_kb,
            "hbm_read_bytes_per_launch": read_b, "hbm_write_bytes_per_launch": write_b,
-           "hbm_bytes_per_launch": read_b + write_b, "algorithmic_bytes_per_launch": algo_bytes,
-           "traffic_over_algorithmic": (read_b + write_b) / algo_bytes,
-           "correction": "read = 2 x FETCH_SIZE x 1024 (gfx950 half-count of wide streaming reads); write = WRITE_SIZE x 1024"}
+           "hbm_bytes_per_launch": read_b + write_b + aux_b, "main_kernel_bytes_per_launch": read_b + write_b,
+           "other_kernels": aux, "other_kernels_bytes_per_launch_raw": aux_b,
+           "algorithmic_bytes_per_launch": algo_bytes,
+           "traffic_over_algorithmic": (read_b + write_b + aux_b) / algo_bytes,
+           "correction": "main kernel: read = 2 x FETCH_SIZE x 1024 (gfx950 half-count of wide streaming reads), "
+                         "write = WRITE_SIZE x 1024; other kernels raw"}
     os.makedirs("profiles", exist_ok=True)
     json.dump(out, open(f"profiles/pmc_{config}.json", "w"), indent=1)
     print(json.dumps(out))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]))
+    main(sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), *sys.argv[5:])
