@@ -201,6 +201,33 @@ __device__ __forceinline__ uint32_t lane_tree_dpp(const uint32_t* lds, uint32_t 
     }
 }
 
+// Raw register of a group from each lane's four dword-stream accumulators (valid in lane 0).
+// Fast path (G <= 16): the final "dword -> register" x^32 is folded into the in-lane products
+// (x^128 = the level-0 tree operator, x^96, x^64, x^32: four independent products, one LDS round
+// trip), then the lane tree via DPP row_shl; the operators commute, so scaling every lane by x^32
+// before the tree equals scaling the tree's result. Wide groups: serial in-lane Horner, a
+// __shfl_xor tree, and the final x^32.
+template <int G>
+__device__ __forceinline__ uint32_t finish_lanes(const uint32_t* lds, uint32_t c0, uint32_t c1, uint32_t c2,
+                                                 uint32_t c3) {
+    using Gm = Geo<G>;
+    if constexpr (Gm::kFast) {
+        const uint32_t v = mul_aux(lds, Gm::kX32Off + 4096u, c0) ^ mul_aux(lds, Gm::kX96Off, c1) ^
+                           mul_aux(lds, Gm::kX64Off, c2) ^ mul_aux(lds, Gm::kX32Off, c3);
+        return lane_tree_dpp<0, Gm::kLevels>(lds, Gm::kX32Off, v);
+    } else {
+        uint32_t v = mul_aux(lds, Gm::kX32Off, c0) ^ c1;
+        v = mul_aux(lds, Gm::kX32Off, v) ^ c2;
+        v = mul_aux(lds, Gm::kX32Off, v) ^ c3;
+#pragma unroll
+        for (int lv = 0; lv < Gm::kLevels; ++lv) {
+            const uint32_t other = (uint32_t)__shfl_xor((int)v, 1 << lv);
+            v = mul_aux(lds, Gm::kX32Off + 4096u * (uint32_t)(1 + lv), v) ^ other;
+        }
+        return mul_aux(lds, Gm::kX32Off, v);
+    }
+}
+
 // Zero the low d bytes (1..15) of a 16-byte little-endian vector.
 __device__ __forceinline__ u32x4 mask_low_bytes(u32x4 w, uint32_t d) {
     auto m = [](uint32_t x, int32_t k) -> uint32_t {  // k = bytes of this dword to clear
@@ -326,23 +353,7 @@ __device__ __forceinline__ uint32_t fold_range(const uint32_t* lds, uint32_t lan
 #undef BKD_FOLD
 #undef BKD_FOLD0
 
-    // Finish: in-lane combine of the 4 streams (x^96, x^64, x^32), lane tree (x^(128*2^s)),
-    // final x^32. Groups inside a DPP row shift with row_shl (VALU latency) instead of ds_bpermute.
-    uint32_t v;
-    if constexpr (Gm::kFast) {
-        v = mul_aux(lds, Gm::kX96Off, c0) ^ mul_aux(lds, Gm::kX64Off, c1) ^ mul_aux(lds, Gm::kX32Off, c2) ^ c3;
-        v = lane_tree_dpp<0, Gm::kLevels>(lds, Gm::kX32Off, v);
-    } else {
-        v = mul_aux(lds, Gm::kX32Off, c0) ^ c1;
-        v = mul_aux(lds, Gm::kX32Off, v) ^ c2;
-        v = mul_aux(lds, Gm::kX32Off, v) ^ c3;
-#pragma unroll
-        for (int lv = 0; lv < Gm::kLevels; ++lv) {
-            const uint32_t other = (uint32_t)__shfl_xor((int)v, 1 << lv);
-            v = mul_aux(lds, Gm::kX32Off + 4096u * (uint32_t)(1 + lv), v) ^ other;
-        }
-    }
-    return mul_aux(lds, Gm::kX32Off, v);
+    return finish_lanes<G>(lds, c0, c1, c2, c3);
 }
 
 // One CRC per work item of `src` (uniform / indexed / framed-payload entries), persistent grid.
@@ -563,21 +574,7 @@ __device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lan
             c3 ^= junk.w;
         }
     }
-    uint32_t v;
-    if constexpr (Gm::kFast) {
-        v = mul_aux(lds, Gm::kX96Off, c0) ^ mul_aux(lds, Gm::kX64Off, c1) ^ mul_aux(lds, Gm::kX32Off, c2) ^ c3;
-        v = lane_tree_dpp<0, Gm::kLevels>(lds, Gm::kX32Off, v);
-    } else {
-        v = mul_aux(lds, Gm::kX32Off, c0) ^ c1;
-        v = mul_aux(lds, Gm::kX32Off, v) ^ c2;
-        v = mul_aux(lds, Gm::kX32Off, v) ^ c3;
-#pragma unroll
-        for (int lv = 0; lv < Gm::kLevels; ++lv) {
-            const uint32_t other = (uint32_t)__shfl_xor((int)v, 1 << lv);
-            v = mul_aux(lds, Gm::kX32Off + 4096u * (uint32_t)(1 + lv), v) ^ other;
-        }
-    }
-    return mul_aux(lds, Gm::kX32Off, v);
+    return finish_lanes<G>(lds, c0, c1, c2, c3);
 }
 
 // Chunk kernel of the ragged-batch plan: one chunk per group, grid stride over the descriptor

@@ -66,20 +66,24 @@ class KernelModel:
         fx = place(s - (wstart + step)) if wstart + step < s + 4 else 0
         if J > 1:
             words[1, 0, 0] ^= fx
+        fast = G <= 16  # finish_lanes(): x^32 folded into the in-lane products, no final multiply
         lane_vals = []
         for g in range(G):
             acc = [int(words[0, g, k]) for k in range(4)]
             for j in range(1, J):
                 acc = [self._mul(self.main, acc[k]) ^ int(words[j, g, k]) for k in range(4)]
-            v = (self._mul(self.x96, acc[0]) ^ self._mul(self.x64, acc[1]) ^ self._mul(self.x32, acc[2])
-                 ^ acc[3])
+            if fast:
+                v = (self._mul(self.lv[0], acc[0]) ^ self._mul(self.x96, acc[1]) ^ self._mul(self.x64, acc[2])
+                     ^ self._mul(self.x32, acc[3]))
+            else:
+                v = self._mul(self.x32, acc[0]) ^ acc[1]
+                v = self._mul(self.x32, v) ^ acc[2]
+                v = self._mul(self.x32, v) ^ acc[3]
             lane_vals.append(v)
         for s in range(self.levels):
-            span = 1 << s
             lane_vals = [self._mul(self.lv[s], lane_vals[2 * m]) ^ lane_vals[2 * m + 1]
                          for m in range(len(lane_vals) // 2)]
-            assert len(lane_vals) == G >> (s + 1) and span
-        total = self._mul(self.x32, lane_vals[0])
+        total = lane_vals[0] if fast else self._mul(self.x32, lane_vals[0])
         return (~total) & 0xFFFFFFFF
 
 
