@@ -453,3 +453,54 @@ def test_zipf_full_size_plan_equals_direct(gpu):
         want = oracle.batch(algo, host, sub_offs, lens[pick])
         assert (plan[pick] == want).all()
     ck.set_plan_mode(0)
+
+
+def test_concurrent_callers(gpu):
+    """§8b threading: one shared library instance called from several host threads at once, each
+    with its own HIP stream (device batches through the plan, the direct kernel and the uniform
+    path) plus host-memory batches that share the staging slots; every result is exact."""
+    import threading
+    import torch
+    rng = np.random.default_rng(21)
+    size = 8_000_000
+    data = oracle.fill_splitmix64(size, 77)
+    base = _dev_bytes(torch, data, gpu)
+    n = 3000
+    lens = rng.integers(0, 20000, n)
+    offs = np.array([rng.integers(0, size - l + 1) for l in lens], dtype=np.int64)
+    seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    want = oracle.batch(ck.CRC32C, data, offs, lens, seeds=seeds)
+    want_u = oracle.uniform(ck.CRC32C, data, 4096, 4096, size // 4096)
+    d_off = torch.from_numpy(offs).to(gpu)
+    d_len = torch.from_numpy(lens.astype(np.int32)).to(gpu)
+    d_seed = torch.from_numpy(seeds.view(np.int32)).to(gpu)
+    torch.cuda.synchronize()
+    errors = []
+
+    def worker(k):
+        try:
+            st = torch.cuda.Stream(device=gpu)
+            for r in range(6):
+                kind = (k + r) % 3
+                if kind == 0:
+                    with torch.cuda.stream(st):
+                        got = ck.crc_batch(ck.CRC32C, base, d_off, d_len, seeds=d_seed, stream=st)
+                    st.synchronize()
+                    assert (got.cpu().numpy().view(np.uint32) == want).all(), ("device", k, r)
+                elif kind == 1:
+                    with torch.cuda.stream(st):
+                        got = ck.crc_batch_uniform(ck.CRC32C, base, 4096, size // 4096, stream=st)
+                    st.synchronize()
+                    assert (got.cpu().numpy().view(np.uint32) == want_u).all(), ("uniform", k, r)
+                else:
+                    got = ck.crc_batch_host(ck.CRC32C, data, offs, lens, seeds=seeds)
+                    assert (got == want).all(), ("host", k, r)
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+
+    threads = [threading.Thread(target=worker, args=(k,)) for k in range(6)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert not errors, errors
