@@ -261,6 +261,9 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
         hipLaunchKernelGGL(bkd::plan_combine_kernel, dim3((unsigned)((n + 1023) / 1024)), dim3(1024), 0, st, base,
                            offsets, lengths, seeds, seed_all, size, n, pg, xtab, tab + 1024, btab, ds.xinv[algo],
                            bkd::gf2::poly(algo), pslot, partials, out, ds.err);
+        hipLaunchKernelGGL(bkd::plan_combine_big_kernel, dim3((unsigned)ds.cus), dim3(256), 0, st, offsets, lengths,
+                           size, pg, xtab, bkd::gf2::xpow(algo, 8ull * pg.ch), ds.xinv[algo], bkd::gf2::poly(algo),
+                           pslot, partials, big, hdr, out);
         e = hipGetLastError();
         if (e != hipSuccess) rc = fail(BKD_ERR_HIP, std::string("plan kernels: ") + hipGetErrorString(e));
     }
@@ -601,22 +604,41 @@ int bkd_resume(int algo, uint32_t current, const void* ptr, uint64_t len, uint32
         DeviceState* ds = nullptr;
         int rc = ensure_current(&ds);
         if (rc) return rc;
-        uint64_t* d_off = nullptr;
-        uint32_t *d_len = nullptr, *d_out = nullptr;
-        BKD_HIP(hipMalloc(&d_off, 8));
-        BKD_HIP(hipMalloc(&d_len, 4));
-        BKD_HIP(hipMalloc(&d_out, 4));
-        BKD_HIP(hipMemcpy(d_off, &off, 8, hipMemcpyHostToDevice));
-        BKD_HIP(hipMemcpy(d_len, &l32, 4, hipMemcpyHostToDevice));
-        rc = indexed_batch(*ds, algo, (const uint8_t*)ptr, len, d_off, d_len, 1, nullptr, current, d_out, nullptr);
-        if (rc == BKD_OK) {
-            hipError_t e = hipMemcpy(out, d_out, 4, hipMemcpyDeviceToHost);
-            if (e != hipSuccess) rc = fail(BKD_ERR_HIP, hipGetErrorString(e));
+        int dev = 0;
+        BKD_HIP(hipGetDevice(&dev));
+        // per-thread, per-device scratch: no allocation (hipFree synchronises the whole device)
+        // and no shared state on this latency path
+        struct CallScratch {
+            hipStream_t st = nullptr;
+            uint32_t* d_out = nullptr;
+            uint64_t* d_off = nullptr;
+            uint32_t* d_len = nullptr;
+            uint32_t* h_out = nullptr;  // pinned: [0] result, [1] length for the plan path
+        };
+        thread_local CallScratch cs[kMaxDevices];
+        CallScratch& c = cs[dev];
+        if (!c.st) {
+            BKD_HIP(hipStreamCreateWithFlags(&c.st, hipStreamNonBlocking));
+            BKD_HIP(hipMalloc((void**)&c.d_out, 4));
+            BKD_HIP(hipMalloc((void**)&c.d_off, 8));
+            BKD_HIP(hipMalloc((void**)&c.d_len, 4));
+            BKD_HIP(hipHostMalloc((void**)&c.h_out, 8, hipHostMallocDefault));
+            BKD_HIP(hipMemsetAsync(c.d_off, 0, 8, c.st));
         }
-        (void)hipFree(d_off);
-        (void)hipFree(d_len);
-        (void)hipFree(d_out);
-        return rc;
+        if (len < (1u << 20)) {  // one group: the entry as a uniform batch of one
+            bkd::UniformSrc src{1, len, l32, nullptr, current, c.d_out};
+            rc = dispatch_lanes(*ds, auto_lanes(len, 1, ds->cus), algo, (const uint8_t*)ptr, src, 1, c.st);
+        } else {  // large: the chunked plan spreads it over the chip
+            c.h_out[1] = l32;
+            BKD_HIP(hipMemcpyAsync(c.d_len, c.h_out + 1, 4, hipMemcpyHostToDevice, c.st));
+            rc = launch_plan(*ds, algo, (const uint8_t*)ptr, len, c.d_off, c.d_len, 1, nullptr, current, c.d_out,
+                             c.st);
+        }
+        if (rc) return rc;
+        BKD_HIP(hipMemcpyAsync(c.h_out, c.d_out, 4, hipMemcpyDeviceToHost, c.st));
+        BKD_HIP(hipStreamSynchronize(c.st));
+        *out = *c.h_out;
+        return BKD_OK;
     }
     return bkd_crc_batch_host(algo, ptr, len, &off, &l32, 1, nullptr, current, out);
 }

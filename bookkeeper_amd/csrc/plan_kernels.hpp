@@ -298,8 +298,31 @@ __global__ void plan_expand_big_kernel(const uint64_t* __restrict__ offsets, con
     }
 }
 
+// a * b mod P, bitwise (no tables): 32 shift/xor steps, for the few products per entry that have
+// no operator table (x^(-8*pad), powers of X).
+__device__ __forceinline__ uint32_t gf_mul_bits(uint32_t a, uint32_t b, uint32_t poly) {
+    uint32_t prod = 0u, cur = b;
+#pragma unroll
+    for (int k = 31; k >= 0; --k) {
+        prod ^= ((a >> k) & 1u) ? cur : 0u;
+        cur = (cur >> 1) ^ ((cur & 1u) ? poly : 0u);
+    }
+    return prod;
+}
+
+__device__ __forceinline__ uint32_t gf_pow_bits(uint32_t x, uint32_t e, uint32_t poly) {
+    uint32_t r = 0x80000000u;  // x^0
+    while (e) {
+        if (e & 1u) r = gf_mul_bits(r, x, poly);
+        x = gf_mul_bits(x, x, poly);
+        e >>= 1;
+    }
+    return r;
+}
+
 // Horner over the partial registers of each chunked entry, then x^(-8*pad); serial fold of
-// entries the plan did not chunk.
+// entries the plan did not chunk. Entries with more than kEmitMax full chunks (the big list) are
+// left to plan_combine_big_kernel.
 __global__ void plan_combine_kernel(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets,
                                     const uint32_t* __restrict__ lengths, const uint32_t* __restrict__ seeds,
                                     uint32_t seed_all, uint64_t size, uint64_t n, PlanGeo pg,
@@ -340,23 +363,56 @@ __global__ void plan_combine_kernel(const uint8_t* __restrict__ base, const uint
         return;
     }
     const EntryPlan p = plan_entry(o, l, size, pg);
+    if (p.full > kEmitMax) return;
     uint32_t reg = partials[slot + p.m - 1u];
     for (int c = (int)p.m - 2; c >= 0; --c) {
         reg = X[reg & 0xffu] ^ X[256 + ((reg >> 8) & 0xffu)] ^ X[512 + ((reg >> 16) & 0xffu)] ^ X[768 + (reg >> 24)];
         reg ^= partials[slot + (uint32_t)c];
     }
     // undo the zero padding: reg * x^(-8*pad), a bitwise product (no table dependency chain)
-    if (p.pad) {
-        const uint32_t k = xinv[p.pad];
-        uint32_t prod = 0u, cur = reg;
-#pragma unroll
-        for (int b = 31; b >= 0; --b) {
-            prod ^= ((k >> b) & 1u) ? cur : 0u;
-            cur = (cur >> 1) ^ ((cur & 1u) ? poly : 0u);
-        }
-        reg = prod;
-    }
+    if (p.pad) reg = gf_mul_bits(xinv[p.pad], reg, poly);
     out[i] = ~reg;
+}
+
+// Combine of the big-list entries (> kEmitMax chunks, e.g. one 64 MiB entry = 16 Ki chunks): one
+// block per entry instead of one serial Horner thread. Thread t folds its contiguous run of
+// partials with Horner (table X in LDS), is placed by X^(first chunk of its run) (bitwise power),
+// and the block XOR-reduces: reg = sum_c partial_c * X^c, then * x^(-8*pad) as in plan_combine.
+__global__ void __launch_bounds__(256) plan_combine_big_kernel(
+    const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ lengths, uint64_t size, PlanGeo pg,
+    const uint32_t* __restrict__ xtab, uint32_t xval, const uint32_t* __restrict__ xinv, uint32_t poly,
+    const uint32_t* __restrict__ pslot, const uint32_t* __restrict__ partials, const uint32_t* __restrict__ big,
+    const uint32_t* __restrict__ hdr, uint32_t* __restrict__ out) {
+    __shared__ uint32_t X[1024];
+    __shared__ uint32_t red[256 / 64];
+    for (int k = threadIdx.x; k < 1024; k += blockDim.x) X[k] = xtab[k];
+    __syncthreads();
+    const uint32_t nbig = hdr[kHdrBig];
+    for (uint32_t k = blockIdx.x; k < nbig; k += gridDim.x) {
+        const uint32_t i = big[k];
+        const uint32_t slot = pslot[i];
+        const EntryPlan p = plan_entry(offsets[i], lengths[i], size, pg);
+        const uint32_t per = (p.m + blockDim.x - 1u) / blockDim.x;
+        const uint32_t lo = threadIdx.x * per;
+        const uint32_t hi = lo + per < p.m ? lo + per : p.m;
+        uint32_t r = 0u;
+        for (int c = (int)hi - 1; c >= (int)lo; --c) {
+            r = X[r & 0xffu] ^ X[256 + ((r >> 8) & 0xffu)] ^ X[512 + ((r >> 16) & 0xffu)] ^ X[768 + (r >> 24)];
+            r ^= partials[slot + (uint32_t)c];
+        }
+        if (lo < hi && lo) r = gf_mul_bits(gf_pow_bits(xval, lo, poly), r, poly);
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) r ^= (uint32_t)__shfl_xor((int)r, d);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = r;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t reg = 0u;
+            for (uint32_t w = 0; w < blockDim.x / 64; ++w) reg ^= red[w];
+            if (p.pad) reg = gf_mul_bits(xinv[p.pad], reg, poly);
+            out[i] = ~reg;
+        }
+        __syncthreads();
+    }
 }
 
 }  // namespace bkd
