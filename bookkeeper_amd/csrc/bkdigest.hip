@@ -261,6 +261,8 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
         hipLaunchKernelGGL(bkd::plan_combine_kernel, dim3((unsigned)((n + 1023) / 1024)), dim3(1024), 0, st, base,
                            offsets, lengths, seeds, seed_all, size, n, pg, xtab, tab + 1024, btab, ds.xinv[algo],
                            bkd::gf2::poly(algo), pslot, partials, out, ds.err);
+        bkd::PlanDirectSrc dsrc{n, offsets, lengths, seeds, seed_all, size, out, pslot, hdr, capacity};
+        if (e == hipSuccess) rc = launch_groups<32>(ds, algo, base, dsrc, n, st);
         hipLaunchKernelGGL(bkd::plan_combine_big_kernel, dim3((unsigned)ds.cus), dim3(256), 0, st, offsets, lengths,
                            size, pg, xtab, bkd::gf2::xpow(algo, 8ull * pg.ch), ds.xinv[algo], bkd::gf2::poly(algo),
                            pslot, partials, big, hdr, out);

@@ -363,6 +363,8 @@ __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __res
                                                             uint32_t* __restrict__ err) {
     using Gm = Geo<G>;
     __shared__ __attribute__((aligned(16))) uint32_t lds[Gm::kLdsWords];
+    const uint64_t n = src.count();
+    if (n == 0) return;  // block-uniform: nothing to do (e.g. the plan's overflow pass when none overflowed)
     stage_tables<G>(lds, tables);
 
     const int lane = threadIdx.x & 63;
@@ -371,7 +373,6 @@ __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __res
     const uint64_t ngroups = (uint64_t)gridDim.x * (kBlock / G);
     const uint64_t gid = (uint64_t)blockIdx.x * (kBlock / G) + (uint64_t)(threadIdx.x / G);
 
-    const uint64_t n = src.count();
     for (uint64_t i = gid; i < n; i += ngroups) {
         Work wk;
         const int st = src.get(i, wk);

@@ -17,9 +17,10 @@
 //  * combines multi-chunk entries as reg = sum_c partial_c * X^c, X = x^(8*CH) (Horner from the
 //    head), then removes the zero padding (multiply by x^(-8*pad)): the GPU analogue of
 //    crc32c_chunk's stream merge by shift tables (crc32c_sse42.cpp:92-134).
-// Entries shorter than 16 bytes, invalid (out-of-bounds) entries, and entries that do not fit the
-// plan's capacity (only possible when entries overlap heavily) are computed serially by
-// plan_combine_kernel (correct, slow path).
+// Entries shorter than 16 bytes and invalid (out-of-bounds) entries are handled by
+// plan_combine_kernel; entries that do not fit the plan's capacity (only possible when entries
+// overlap heavily) are computed by the one-entry-per-group kernel over PlanDirectSrc, a pass that
+// exits at once when nothing overflowed.
 //
 // Launch sequence (caller's stream, no host sync): plan_count -> plan_scan -> plan_emit ->
 // plan_expand_big -> crc_plan_chunks_kernel -> plan_combine.
@@ -281,6 +282,31 @@ __global__ void __launch_bounds__(kPlanBlock) plan_emit_kernel(const uint64_t* _
     }
 }
 
+// Entries the plan could not hold (pslot == kDirect): one entry per lane group, like IndexedSrc.
+// count() is 0 unless the plan overflowed (total chunks > capacity), so the pass is free otherwise.
+struct PlanDirectSrc {
+    uint64_t n;
+    const uint64_t* offsets;
+    const uint32_t* lengths;
+    const uint32_t* seeds;
+    uint32_t seed_all;
+    uint64_t size;
+    uint32_t* out;
+    const uint32_t* pslot;
+    const uint32_t* hdr;
+    uint64_t capacity;
+    __device__ __forceinline__ uint64_t count() const { return (uint64_t)hdr[kHdrTotal] > capacity ? n : 0u; }
+    __device__ __forceinline__ int get(uint64_t i, Work& w) const {
+        if (pslot[i] != kDirect) return 3;
+        w.dst = out + i;
+        w.s = (int64_t)offsets[i];
+        w.len = lengths[i];
+        w.r0 = ~(seeds ? seeds[i] : seed_all);
+        w.xorout = 0xFFFFFFFFu;
+        return 0;
+    }
+};
+
 // Full-bucket descriptors of entries with more than kEmitMax chunks: one block per entry.
 __global__ void plan_expand_big_kernel(const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ lengths,
                                        const uint32_t* __restrict__ seeds, uint32_t seed_all, uint64_t size, PlanGeo pg,
@@ -348,7 +374,8 @@ __global__ void plan_combine_kernel(const uint8_t* __restrict__ base, const uint
         if (err) atomicOr(err, 1u);
         return;
     }
-    if (slot == kSerial || slot == kDirect) {
+    if (slot == kDirect) return;  // the overflow pass (PlanDirectSrc) computes it
+    if (slot == kSerial) {
         uint32_t reg = ~(seeds ? seeds[i] : seed_all);
         const uint8_t* q = base + o;
         const uint8_t* qe = q + l;
