@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <atomic>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -43,6 +44,46 @@ int lane_index(int lanes) {
     return -1;
 }
 
+// Stream-ordered scratch kept per (device, stream) between calls. A call's kernels use it in
+// stream order, so consecutive calls on one stream can share it; the launch sequence is enqueued
+// under `mu` so that host threads sharing a stream do not interleave their sequences. It only
+// grows (old buffer released with hipFreeAsync on the same stream). Per-call hipMallocAsync /
+// hipFreeAsync left the GPU idle ~40 us between calls (profiles/r01_diag_ragged.log).
+struct StreamScratch {
+    std::recursive_mutex mu;
+    uint8_t* buf[2] = {};  // slot 0: plan scratch (launch_plan), slot 1: verify pipeline
+    size_t cap[2] = {};
+    // Returns slot `which` with at least `bytes` bytes, stream-ordered on `st`.
+    hipError_t get(int which, size_t bytes, hipStream_t st, uint8_t** out) {
+        if (cap[which] < bytes) {
+            if (buf[which]) (void)hipFreeAsync(buf[which], st);
+            buf[which] = nullptr;
+            cap[which] = 0;
+            const size_t want = bytes + bytes / 4 + 4096;
+            hipError_t e = hipMallocAsync((void**)&buf[which], want, st);
+            if (e != hipSuccess) return e;
+            cap[which] = want;
+        }
+        *out = buf[which];
+        return hipSuccess;
+    }
+};
+
+// Lays out 256-byte-aligned sub-buffers of one scratch allocation: take() returns offsets
+// during the sizing pass; at(base, off) turns them into pointers.
+struct Carver {
+    size_t used = 0;
+    size_t take(size_t bytes) {
+        const size_t at = used;
+        used += (bytes + 255) & ~(size_t)255;
+        return at;
+    }
+    template <class T>
+    static T* at(uint8_t* base, size_t off) {
+        return reinterpret_cast<T*>(base + off);
+    }
+};
+
 struct DeviceState {
     bool ready = false;
     int cus = 0;
@@ -50,6 +91,7 @@ struct DeviceState {
     uint32_t* err = nullptr;      // sticky bounds-violation flag for indexed batches
     uint32_t* xinv[2] = {};       // [algo] x^(-8k), k = 0..127: removes the plan's zero padding
     std::map<uint64_t, uint32_t*> xtab;  // (algo, CH) -> x^(8*CH) operator for the plan's combine
+    std::map<hipStream_t, std::unique_ptr<StreamScratch>> scratch;
 };
 
 std::mutex g_mu;
@@ -142,6 +184,13 @@ int ensure_current(DeviceState** out) {
     return BKD_OK;
 }
 
+StreamScratch& scratch_for(DeviceState& ds, hipStream_t st) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto& slot = ds.scratch[st];
+    if (!slot) slot.reset(new StreamScratch());
+    return *slot;
+}
+
 // Lanes per entry group for the direct kernel, from the size sweep (profiles/r01_size_sweep.log):
 // 4 lanes below 512 B, 8 up to 32 KiB, 32 above; then more lanes while the batch would not give
 // every lane slot of the chip (CUs x 1024) one group lane, so a few huge entries still fill it.
@@ -228,17 +277,20 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     const uint64_t capacity = std::min<uint64_t>(n + (size + 128u * n) / pg.ch + 16, 0xFFFFFFF0ull);
     const uint32_t nb = (uint32_t)((n + bkd::kPlanBlock - 1) / bkd::kPlanBlock);
     const uint32_t ncols = pg.nbins + 1u;
-    uint32_t *blk = nullptr, *blkoff = nullptr, *hdr = nullptr, *run_start = nullptr, *pslot = nullptr,
-             *big = nullptr, *partials = nullptr;
-    bkd::PlanDesc* descs = nullptr;
-    hipError_t e = hipMallocAsync((void**)&blk, (size_t)nb * ncols * 4, st);
-    if (e == hipSuccess) e = hipMallocAsync((void**)&blkoff, (size_t)nb * ncols * 4, st);
-    if (e == hipSuccess) e = hipMallocAsync((void**)&hdr, bkd::kHdrWords * 4, st);
-    if (e == hipSuccess) e = hipMallocAsync((void**)&run_start, (size_t)n * 4, st);
-    if (e == hipSuccess) e = hipMallocAsync((void**)&pslot, (size_t)n * 4, st);
-    if (e == hipSuccess) e = hipMallocAsync((void**)&big, (size_t)n * 4, st);
-    if (e == hipSuccess) e = hipMallocAsync((void**)&partials, (size_t)capacity * 4, st);
-    if (e == hipSuccess) e = hipMallocAsync((void**)&descs, (size_t)capacity * sizeof(bkd::PlanDesc), st);
+    Carver cv;
+    const size_t o_blk = cv.take((size_t)nb * ncols * 4), o_blkoff = cv.take((size_t)nb * ncols * 4),
+                 o_hdr = cv.take(bkd::kHdrWords * 4), o_rs = cv.take((size_t)n * 4), o_ps = cv.take((size_t)n * 4),
+                 o_big = cv.take((size_t)n * 4), o_part = cv.take((size_t)capacity * 4),
+                 o_desc = cv.take((size_t)capacity * sizeof(bkd::PlanDesc));
+    StreamScratch& sc = scratch_for(ds, st);
+    std::lock_guard<std::recursive_mutex> lk(sc.mu);
+    uint8_t* sb = nullptr;
+    hipError_t e = sc.get(0, cv.used, st, &sb);
+    uint32_t *blk = Carver::at<uint32_t>(sb, o_blk), *blkoff = Carver::at<uint32_t>(sb, o_blkoff),
+             *hdr = Carver::at<uint32_t>(sb, o_hdr), *run_start = Carver::at<uint32_t>(sb, o_rs),
+             *pslot = Carver::at<uint32_t>(sb, o_ps), *big = Carver::at<uint32_t>(sb, o_big),
+             *partials = Carver::at<uint32_t>(sb, o_part);
+    bkd::PlanDesc* descs = Carver::at<bkd::PlanDesc>(sb, o_desc);
     if (e != hipSuccess) {
         rc = fail(BKD_ERR_NOMEM, std::string("plan scratch: ") + hipGetErrorString(e));
     } else {
@@ -269,9 +321,6 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
         e = hipGetLastError();
         if (e != hipSuccess) rc = fail(BKD_ERR_HIP, std::string("plan kernels: ") + hipGetErrorString(e));
     }
-    for (void* p : {(void*)blk, (void*)blkoff, (void*)hdr, (void*)run_start, (void*)pslot, (void*)big,
-                    (void*)partials, (void*)descs})
-        if (p) (void)hipFreeAsync(p, st);
     return rc;
 }
 
@@ -696,11 +745,15 @@ int verify_framed(int algo, int64_t ledger_id, int64_t first_entry_id, int id_ch
     }
     const uint32_t* btab = ds->tables[algo][lane_index(4)] + bkd::gf2::byte_table_offset(4);
     const unsigned blocks = (unsigned)((n + 255) / 256);
-    uint32_t *seeds = nullptr, *plen = nullptr;
-    uint64_t* poff = nullptr;
-    hipError_t e = hipMallocAsync((void**)&seeds, n * 4, st);
-    if (e == hipSuccess) e = hipMallocAsync((void**)&plen, n * 4, st);
-    if (e == hipSuccess) e = hipMallocAsync((void**)&poff, n * 8, st);
+    Carver cv;
+    const size_t o_seeds = cv.take(n * 4), o_plen = cv.take(n * 4), o_poff = cv.take(n * 8);
+    StreamScratch& sc = scratch_for(*ds, st);
+    std::lock_guard<std::recursive_mutex> lk(sc.mu);  // held across the nested plan (slot 0)
+    uint8_t* sb = nullptr;
+    hipError_t e = sc.get(1, cv.used, st, &sb);
+    uint32_t* seeds = Carver::at<uint32_t>(sb, o_seeds);
+    uint32_t* plen = Carver::at<uint32_t>(sb, o_plen);
+    uint64_t* poff = Carver::at<uint64_t>(sb, o_poff);
     if (e != hipSuccess) {
         rc = fail(BKD_ERR_NOMEM, std::string("verify scratch: ") + hipGetErrorString(e));
     } else {
@@ -720,8 +773,6 @@ int verify_framed(int algo, int64_t ledger_id, int64_t first_entry_id, int id_ch
             if (e != hipSuccess) rc = fail(BKD_ERR_HIP, hipGetErrorString(e));
         }
     }
-    for (void* p : {(void*)seeds, (void*)plen, (void*)poff})
-        if (p) (void)hipFreeAsync(p, st);
     return rc;
 }
 }  // namespace
