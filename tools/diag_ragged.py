@@ -5,6 +5,7 @@ then `python3 tools/diag_ragged.py --report DIR/diag_kernel_trace.csv`. Workload
 the trace by a marker launch (fill_splitmix64 on a 64-byte buffer); their order is WORKLOADS'.
 """
 import csv
+import re
 import os
 import sys
 from collections import defaultdict
@@ -71,8 +72,23 @@ def run():
         "zipf_lt1k_direct": direct_idx(lo, ll),
         "zipf_plan_crc32": plan(algo=1),
     }
-    info = {"zipf_ge4k_plan": (int(ge.sum()), int(lens[ge].sum())), "zipf_lt1k_plan": (int(lt.sum()), int(lens[lt].sum())),
+    # packed{S}_{plan|direct|plan4}: n entries of S bytes back to back (unaligned starts)
+    info_pk = {}
+    for name in WORKLOADS:
+        m = re.match(r"packed(\d+)_(plan4|plan|direct)$", name)
+        if not m:
+            continue
+        S = int(m.group(1))
+        npk = min(n, base.numel() // S)
+        po, pl = indexed(np.arange(npk, dtype=np.int64) * S, np.full(npk, S))
+        info_pk[name] = (npk, npk * S)
+        kind = m.group(2)
+        jobs[name] = (direct_idx(po, pl) if kind == "direct" else
+                      plan(o=po, l=pl, geom=(4, 64, 16) if kind == "plan4" else (8, 32, 16)))
+    info = {"zipf_ge4k_plan": (int(ge.sum()), int(lens[ge].sum())),
+            "zipf_ge4k_plan_o0": (int(ge.sum()), int(lens[ge].sum())), "zipf_lt1k_plan": (int(lt.sum()), int(lens[lt].sum())),
             "zipf_lt1k_direct": (int(lt.sum()), int(lens[lt].sum()))}
+    info.update(info_pk)
     ref = {}
     for name in WORKLOADS:
         f = jobs[name]
