@@ -243,20 +243,21 @@ int dispatch_lanes(DeviceState& ds, int lanes, int algo, const uint8_t* base, co
 
 template <int G>
 void launch_plan_chunks(const uint8_t* base, const bkd::PlanDesc* descs, const uint32_t* count, const uint32_t* tab,
-                        uint32_t* out, uint32_t* partials, int blocks, hipStream_t st) {
+                        uint32_t* out, uint32_t* partials, const bkd::PlanDirectSrc& ov, int blocks, hipStream_t st) {
     const int pf = g_plan_pf.load();
     if (pf == 8)
-        hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 8, kNT>), dim3((unsigned)blocks), dim3(bkd::kBlock), 0, st,
-                           base, descs, count, tab, out, partials);
+        hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 8, kNT, bkd::PlanDirectSrc>), dim3((unsigned)blocks),
+                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov);
     else if (pf == 4)
-        hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 4, kNT>), dim3((unsigned)blocks), dim3(bkd::kBlock), 0, st,
-                           base, descs, count, tab, out, partials);
+        hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 4, kNT, bkd::PlanDirectSrc>), dim3((unsigned)blocks),
+                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov);
     else
-        hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 2, kNT>), dim3((unsigned)blocks), dim3(bkd::kBlock), 0, st,
-                           base, descs, count, tab, out, partials);
+        hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 2, kNT, bkd::PlanDirectSrc>), dim3((unsigned)blocks),
+                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov);
 }
 
-// Indexed batch through the chunked plan (plan_kernels.hpp). Scratch is stream-ordered.
+// Indexed batch through the chunked plan (plan_kernels.hpp): five stream-ordered kernels, no
+// host sync, scratch from the stream's arena.
 int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, const uint64_t* offsets,
                 const uint32_t* lengths, uint64_t n, const uint32_t* seeds, uint32_t seed_all, uint32_t* out,
                 hipStream_t st) {
@@ -270,6 +271,8 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     pg.mis = (uint32_t)((uintptr_t)base & 127u);
     pg.merge = (uint32_t)g_plan_merge.load();
     pg.nbins = (pg.ch + pg.merge - 1u + pg.step - 1u) / pg.step + 1u;
+    pg.step_sh = (uint32_t)__builtin_ctz(pg.step);
+    pg.ch_sh = (pg.ch & (pg.ch - 1u)) == 0u ? (uint32_t)__builtin_ctz(pg.ch) : 0xFFu;
     const uint32_t* xtab = nullptr;
     int rc = xtab_for(ds, algo, pg.ch, &xtab);
     if (rc) return rc;
@@ -278,50 +281,40 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     const uint32_t nb = (uint32_t)((n + bkd::kPlanBlock - 1) / bkd::kPlanBlock);
     const uint32_t ncols = pg.nbins + 1u;
     Carver cv;
-    const size_t o_blk = cv.take((size_t)nb * ncols * 4), o_blkoff = cv.take((size_t)nb * ncols * 4),
-                 o_hdr = cv.take(bkd::kHdrWords * 4), o_rs = cv.take((size_t)n * 4), o_ps = cv.take((size_t)n * 4),
-                 o_big = cv.take((size_t)n * 4), o_part = cv.take((size_t)capacity * 4),
+    const size_t o_blk = cv.take((size_t)nb * ncols * 4),
+                 o_blkoff = cv.take((size_t)nb * ncols * 4), o_hdr = cv.take(bkd::kHdrWords * 4),
+                 o_ps = cv.take((size_t)n * 4), o_part = cv.take((size_t)capacity * 4),
                  o_desc = cv.take((size_t)capacity * sizeof(bkd::PlanDesc));
     StreamScratch& sc = scratch_for(ds, st);
     std::lock_guard<std::recursive_mutex> lk(sc.mu);
     uint8_t* sb = nullptr;
     hipError_t e = sc.get(0, cv.used, st, &sb);
-    uint32_t *blk = Carver::at<uint32_t>(sb, o_blk), *blkoff = Carver::at<uint32_t>(sb, o_blkoff),
-             *hdr = Carver::at<uint32_t>(sb, o_hdr), *run_start = Carver::at<uint32_t>(sb, o_rs),
-             *pslot = Carver::at<uint32_t>(sb, o_ps), *big = Carver::at<uint32_t>(sb, o_big),
-             *partials = Carver::at<uint32_t>(sb, o_part);
+    if (e != hipSuccess) return fail(BKD_ERR_NOMEM, std::string("plan scratch: ") + hipGetErrorString(e));
+    uint32_t *blk = Carver::at<uint32_t>(sb, o_blk),
+             *blkoff = Carver::at<uint32_t>(sb, o_blkoff), *hdr = Carver::at<uint32_t>(sb, o_hdr),
+             *pslot = Carver::at<uint32_t>(sb, o_ps), *partials = Carver::at<uint32_t>(sb, o_part);
     bkd::PlanDesc* descs = Carver::at<bkd::PlanDesc>(sb, o_desc);
-    if (e != hipSuccess) {
-        rc = fail(BKD_ERR_NOMEM, std::string("plan scratch: ") + hipGetErrorString(e));
-    } else {
-        hipLaunchKernelGGL(bkd::plan_count_kernel, dim3(nb), dim3(bkd::kPlanBlock), 0, st, offsets, lengths, size, n,
-                           pg, blk, hdr);
-        hipLaunchKernelGGL(bkd::plan_scan_kernel, dim3(ncols), dim3(64), 0, st, blk, nb, blkoff, hdr);
-        hipLaunchKernelGGL(bkd::plan_emit_kernel, dim3(nb), dim3(bkd::kPlanBlock), 0, st, offsets, lengths, seeds,
-                           seed_all, size, n, pg, capacity, blkoff, pslot, run_start, big, hdr, descs);
-        hipLaunchKernelGGL(bkd::plan_expand_big_kernel, dim3((unsigned)ds.cus), dim3(256), 0, st, offsets, lengths,
-                           seeds, seed_all, size, pg, pslot, run_start, big, hdr, descs);
-        const uint32_t* tab = ds.tables[algo][lane_index(G)];
-        switch (G) {
-            case 4: launch_plan_chunks<4>(base, descs, hdr + bkd::kHdrWork, tab, out, partials, ds.cus, st); break;
-            case 8: launch_plan_chunks<8>(base, descs, hdr + bkd::kHdrWork, tab, out, partials, ds.cus, st); break;
-            case 16: launch_plan_chunks<16>(base, descs, hdr + bkd::kHdrWork, tab, out, partials, ds.cus, st); break;
-            case 32: launch_plan_chunks<32>(base, descs, hdr + bkd::kHdrWork, tab, out, partials, ds.cus, st); break;
-            default: launch_plan_chunks<64>(base, descs, hdr + bkd::kHdrWork, tab, out, partials, ds.cus, st); break;
-        }
-        const uint32_t* btab = tab + bkd::gf2::byte_table_offset(G);
-        hipLaunchKernelGGL(bkd::plan_combine_kernel, dim3((unsigned)((n + 1023) / 1024)), dim3(1024), 0, st, base,
-                           offsets, lengths, seeds, seed_all, size, n, pg, xtab, tab + 1024, btab, ds.xinv[algo],
-                           bkd::gf2::poly(algo), pslot, partials, out, ds.err);
-        bkd::PlanDirectSrc dsrc{n, offsets, lengths, seeds, seed_all, size, out, pslot, hdr, capacity};
-        if (e == hipSuccess) rc = launch_groups<32>(ds, algo, base, dsrc, n, st);
-        hipLaunchKernelGGL(bkd::plan_combine_big_kernel, dim3((unsigned)ds.cus), dim3(256), 0, st, offsets, lengths,
-                           size, pg, xtab, bkd::gf2::xpow(algo, 8ull * pg.ch), ds.xinv[algo], bkd::gf2::poly(algo),
-                           pslot, partials, big, hdr, out);
-        e = hipGetLastError();
-        if (e != hipSuccess) rc = fail(BKD_ERR_HIP, std::string("plan kernels: ") + hipGetErrorString(e));
+    hipLaunchKernelGGL(bkd::plan_count_kernel, dim3(nb), dim3(bkd::kPlanBlock), 0, st, offsets, lengths, size, n, pg,
+                       blk);
+    hipLaunchKernelGGL(bkd::plan_scan_kernel, dim3(ncols), dim3(64), 0, st, blk, nb, blkoff, hdr);
+    hipLaunchKernelGGL(bkd::plan_emit_kernel, dim3(nb), dim3(bkd::kPlanBlock), 0, st, offsets, lengths, seeds,
+                       seed_all, size, n, pg, capacity, blkoff, pslot, hdr, descs);
+    const uint32_t* tab = ds.tables[algo][lane_index(G)];
+    const bkd::PlanDirectSrc ov{n, offsets, lengths, seeds, seed_all, size, out, pslot, hdr, capacity};
+    switch (G) {
+        case 4: launch_plan_chunks<4>(base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st); break;
+        case 8: launch_plan_chunks<8>(base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st); break;
+        case 16: launch_plan_chunks<16>(base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st); break;
+        case 32: launch_plan_chunks<32>(base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st); break;
+        default: launch_plan_chunks<64>(base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st); break;
     }
-    return rc;
+    const uint32_t* btab = tab + bkd::gf2::byte_table_offset(G);
+    hipLaunchKernelGGL(bkd::plan_combine_kernel, dim3(nb), dim3(1024), 0, st, base, offsets, lengths, seeds, seed_all,
+                       size, n, pg, xtab, bkd::gf2::xpow(algo, 8ull * pg.ch), tab + 1024, btab, ds.xinv[algo],
+                       bkd::gf2::poly(algo), pslot, partials, out, ds.err);
+    e = hipGetLastError();
+    if (e != hipSuccess) return fail(BKD_ERR_HIP, std::string("plan kernels: ") + hipGetErrorString(e));
+    return BKD_OK;
 }
 
 int indexed_batch(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, const uint64_t* offsets,

@@ -356,23 +356,12 @@ __device__ __forceinline__ uint32_t fold_range(const uint32_t* lds, uint32_t lan
     return finish_lanes<G>(lds, c0, c1, c2, c3);
 }
 
-// One CRC per work item of `src` (uniform / indexed / framed-payload entries), persistent grid.
+// Grid-stride loop of the one-entry-per-group kernels: work items gid, gid + ngroups, ... of `src`.
 template <int G, int PF, bool NT, class Src>
-__global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __restrict__ base, Src src,
-                                                            const uint32_t* __restrict__ tables,
-                                                            uint32_t* __restrict__ err) {
+__device__ __forceinline__ void groups_loop(const uint32_t* lds, uint32_t lanereg, int g,
+                                            const uint8_t* __restrict__ base, const Src& src, uint64_t n,
+                                            uint64_t gid, uint64_t ngroups, uint32_t* __restrict__ err) {
     using Gm = Geo<G>;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[Gm::kLdsWords];
-    const uint64_t n = src.count();
-    if (n == 0) return;  // block-uniform: nothing to do (e.g. the plan's overflow pass when none overflowed)
-    stage_tables<G>(lds, tables);
-
-    const int lane = threadIdx.x & 63;
-    const int g = lane & (G - 1);
-    const uint32_t lanereg = ((uint32_t)(lane & 31) << 2) | (1u << 16);
-    const uint64_t ngroups = (uint64_t)gridDim.x * (kBlock / G);
-    const uint64_t gid = (uint64_t)blockIdx.x * (kBlock / G) + (uint64_t)(threadIdx.x / G);
-
     for (uint64_t i = gid; i < n; i += ngroups) {
         Work wk;
         const int st = src.get(i, wk);
@@ -397,6 +386,25 @@ __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __res
             fold_range<G, PF, NT, false>(lds, lanereg, g, base, wk.s, wk.s + (int64_t)wk.len, wk.r0);
         if (g == 0) *wk.dst = v ^ wk.xorout;
     }
+}
+
+// One CRC per work item of `src` (uniform / indexed / framed-payload entries), persistent grid.
+template <int G, int PF, bool NT, class Src>
+__global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __restrict__ base, Src src,
+                                                            const uint32_t* __restrict__ tables,
+                                                            uint32_t* __restrict__ err) {
+    using Gm = Geo<G>;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[Gm::kLdsWords];
+    const uint64_t n = src.count();
+    if (n == 0) return;
+    stage_tables<G>(lds, tables);
+
+    const int lane = threadIdx.x & 63;
+    const int g = lane & (G - 1);
+    const uint32_t lanereg = ((uint32_t)(lane & 31) << 2) | (1u << 16);
+    const uint64_t ngroups = (uint64_t)gridDim.x * (kBlock / G);
+    const uint64_t gid = (uint64_t)blockIdx.x * (kBlock / G) + (uint64_t)(threadIdx.x / G);
+    groups_loop<G, PF, NT>(lds, lanereg, g, base, src, n, gid, ngroups, err);
 }
 
 // ---- chunk descriptors of the ragged-batch plan (built by plan_kernels.hpp) ----
@@ -578,29 +586,12 @@ __device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lan
     return finish_lanes<G>(lds, c0, c1, c2, c3);
 }
 
-// Chunk kernel of the ragged-batch plan: one chunk per group, grid stride over the descriptor
-// list (sorted by step count, plan_kernels.hpp). Descriptors are read two rounds ahead and each
-// chunk's first loads are issued during the previous chunk (chunk_fold), X/Y register sets
-// alternating.
+// The chunk list [0, n) in grid stride (crc_plan_chunks_kernel).
 template <int G, int PF, bool NT>
-__global__ void __launch_bounds__(kBlock) crc_plan_chunks_kernel(const uint8_t* __restrict__ base,
-                                                                 const PlanDesc* __restrict__ descs,
-                                                                 const uint32_t* __restrict__ count,
-                                                                 const uint32_t* __restrict__ tables,
-                                                                 uint32_t* __restrict__ out,
-                                                                 uint32_t* __restrict__ partials) {
-    using Gm = Geo<G>;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[Gm::kLdsWords];
-    stage_tables<G>(lds, tables);
-
-    const int lane = threadIdx.x & 63;
-    const int g = lane & (G - 1);
-    const uint32_t lanereg = ((uint32_t)(lane & 31) << 2) | (1u << 16);
-    const uint64_t ngroups = (uint64_t)gridDim.x * (kBlock / G);
-    const uint64_t gid = (uint64_t)blockIdx.x * (kBlock / G) + (uint64_t)(threadIdx.x / G);
-    const uint64_t n = *count;
-    if (gid >= n) return;
-
+__device__ __forceinline__ void plan_chunks_loop(const uint32_t* lds, uint32_t lanereg, int g,
+                                                 const uint8_t* __restrict__ base, const PlanDesc* __restrict__ descs,
+                                                 uint64_t n, uint64_t gid, uint64_t ngroups, uint32_t* __restrict__ out,
+                                                 uint32_t* __restrict__ partials) {
     auto clampi = [&](uint64_t j) { return j < n ? j : n - 1; };
     // a hole (len == 0) or a missing next chunk prefetches the current chunk's own blocks
     auto pf_geo = [&](const ChunkGeo& nx, const ChunkGeo& cur) -> const ChunkGeo& { return nx.len ? nx : cur; };
@@ -650,6 +641,33 @@ __global__ void __launch_bounds__(kBlock) crc_plan_chunks_kernel(const uint8_t* 
             dn = dnn;
         }
     }
+}
+
+// Chunk kernel of the ragged-batch plan: one chunk per group, grid stride over the descriptor
+// list (sorted by step count, plan_kernels.hpp). Descriptors are read two rounds ahead and each
+// chunk's first loads are issued during the previous chunk (chunk_fold), X/Y register sets
+// alternating.
+// After its chunks, the grid computes the entries the plan could not hold (`ov`, normally empty).
+template <int G, int PF, bool NT, class OvSrc>
+__global__ void __launch_bounds__(kBlock) crc_plan_chunks_kernel(const uint8_t* __restrict__ base,
+                                                                 const PlanDesc* __restrict__ descs,
+                                                                 const uint32_t* __restrict__ count,
+                                                                 const uint32_t* __restrict__ tables,
+                                                                 uint32_t* __restrict__ out,
+                                                                 uint32_t* __restrict__ partials, OvSrc ov) {
+    using Gm = Geo<G>;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[Gm::kLdsWords];
+    stage_tables<G>(lds, tables);
+
+    const int lane = threadIdx.x & 63;
+    const int g = lane & (G - 1);
+    const uint32_t lanereg = ((uint32_t)(lane & 31) << 2) | (1u << 16);
+    const uint64_t ngroups = (uint64_t)gridDim.x * (kBlock / G);
+    const uint64_t gid = (uint64_t)blockIdx.x * (kBlock / G) + (uint64_t)(threadIdx.x / G);
+    const uint64_t n = *count;
+    if (gid < n) plan_chunks_loop<G, PF, NT>(lds, lanereg, g, base, descs, n, gid, ngroups, out, partials);
+    const uint64_t nov = ov.count();
+    if (nov) groups_loop<G, PF, NT>(lds, lanereg, g, base, ov, nov, gid, ngroups, nullptr);
 }
 
 // ---- synthetic input: little-endian splitmix64 stream ----

@@ -19,11 +19,11 @@
 //    crc32c_chunk's stream merge by shift tables (crc32c_sse42.cpp:92-134).
 // Entries shorter than 16 bytes and invalid (out-of-bounds) entries are handled by
 // plan_combine_kernel; entries that do not fit the plan's capacity (only possible when entries
-// overlap heavily) are computed by the one-entry-per-group kernel over PlanDirectSrc, a pass that
-// exits at once when nothing overflowed.
+// overlap heavily) are computed one entry per lane group (PlanDirectSrc) in the tail of the chunk
+// kernel, a loop that is skipped when nothing overflowed.
 //
 // Launch sequence (caller's stream, no host sync): plan_count -> plan_scan -> plan_emit ->
-// plan_expand_big -> crc_plan_chunks_kernel -> plan_combine.
+// crc_plan_chunks_kernel (+ overflow tail) -> plan_combine.
 #pragma once
 #include "crc_kernels.hpp"
 
@@ -31,7 +31,6 @@ namespace bkd {
 
 constexpr int kPlanBlock = 1024;
 constexpr int kMaxJC = 256;  // bins 0 .. jc + merge steps
-constexpr uint32_t kEmitMax = 64;  // an emit thread writes at most this many full-chunk descriptors
 
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;  // single aligned chunk, no tail: the chunk writes out[] itself
 constexpr uint32_t kSerial = 0xFFFFFFFEu;  // whole entry folded serially by the combine kernel
@@ -44,13 +43,14 @@ struct PlanGeo {
     uint32_t mis;    // device address of base modulo 128
     uint32_t merge;  // a head chunk shorter than this (>= 16) merges into its neighbour
     uint32_t nbins;  // bins 0 .. nbins-1: ceil((ch + merge - 1) / step) + 1
+    uint32_t step_sh;  // log2(step)
+    uint32_t ch_sh;    // log2(ch) when ch is a power of two, else 0xFF (64-bit divisions are slow)
 };
 
 // hdr words
 constexpr int kHdrTotal = 0;  // all chunks
 constexpr int kHdrSlots = 1;  // partial slots
 constexpr int kHdrWork = 2;   // descriptors to process = min(total, capacity)
-constexpr int kHdrBig = 3;    // entries whose full chunks plan_expand_big writes
 constexpr int kHdrBase = 4;   // kHdrBase + col: total of column col (plan_scan)
 constexpr int kHdrWords = kHdrBase + kMaxJC + 2;
 
@@ -88,14 +88,14 @@ __device__ __forceinline__ EntryPlan plan_entry(uint64_t o, uint32_t l, uint64_t
     p.pad = (uint32_t)((al - ((pg.mis + (uint64_t)p.e) & (al - 1u))) & (al - 1u));
     p.ae = p.e + (int64_t)p.pad;
     const uint64_t la = (uint64_t)(p.ae - p.s);
-    uint32_t m = (uint32_t)((la + pg.ch - 1) / pg.ch);
-    uint64_t hl = la - (uint64_t)(m - 1u) * pg.ch;
+    uint32_t m = pg.ch_sh < 32u ? (uint32_t)((la + pg.ch - 1) >> pg.ch_sh) : (uint32_t)((la + pg.ch - 1) / pg.ch);
+    uint32_t hl = (uint32_t)(la - (uint64_t)(m - 1u) * pg.ch);
     if (hl < pg.merge && m > 1u) {  // a short head merges into its neighbour (up to ch + merge - 1 bytes)
         --m;
         hl += pg.ch;
     }
     p.m = m;
-    p.jh = (uint32_t)((hl + pg.step - 1) / pg.step);
+    p.jh = (hl + pg.step - 1u) >> pg.step_sh;
     p.full = (m - 1u) + (p.jh == pg.jc ? 1u : 0u);
     p.ps = (m == 1u && p.pad == 0u) ? 0u : m;
     p.kind = 0;
@@ -148,12 +148,11 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
 __device__ __forceinline__ uint32_t plan_ncols(const PlanGeo& pg) { return pg.nbins + 1u; }
 __device__ __forceinline__ uint32_t slot_col(const PlanGeo& pg) { return pg.nbins; }
 
+// Per-block column counts (plan_scan_kernel turns them into per-block offsets and totals).
 __global__ void __launch_bounds__(kPlanBlock) plan_count_kernel(const uint64_t* __restrict__ offsets,
                                                                 const uint32_t* __restrict__ lengths, uint64_t size,
-                                                                uint64_t n, PlanGeo pg, uint32_t* __restrict__ blk,
-                                                                uint32_t* __restrict__ hdr) {
+                                                                uint64_t n, PlanGeo pg, uint32_t* __restrict__ blk) {
     __shared__ uint32_t col[kMaxJC + 2];
-    if (blockIdx.x == 0 && threadIdx.x == 0) hdr[kHdrBig] = 0;
     const uint32_t ncols = plan_ncols(pg);
     for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) col[k] = 0u;
     __syncthreads();
@@ -184,6 +183,8 @@ __global__ void __launch_bounds__(kPlanBlock) plan_count_kernel(const uint64_t* 
 // One 64-lane block per column: exclusive scan of the column's per-block counts across blocks
 // (coalesced, 16 rows per lane in flight, carry in a register); the column total goes to
 // hdr[kHdrBase + col]. plan_emit places the bins (descending step count) from those totals.
+// (Folding this scan into the count kernel's last block needs a device-scope release per block,
+// an L2 write-back on this multi-XCD part: measured 52 us instead of 7.5 + 5.8.)
 __global__ void __launch_bounds__(64) plan_scan_kernel(const uint32_t* __restrict__ blk, uint32_t nb,
                                                        uint32_t* __restrict__ blkoff, uint32_t* __restrict__ hdr) {
     const uint32_t c = blockIdx.x;
@@ -214,17 +215,35 @@ __global__ void __launch_bounds__(64) plan_scan_kernel(const uint32_t* __restric
     if (lane == 0) hdr[kHdrBase + c] = carry;
 }
 
+// Descriptor of chunk c of an entry from its stashed plan (plan_emit's cooperative pass).
+__device__ __forceinline__ PlanDesc chunk_desc_of(int64_t ae, int64_t s0, uint32_t m, uint32_t pad, bool final,
+                                                  uint32_t c, uint32_t seed, uint32_t entry, uint32_t slot,
+                                                  const PlanGeo& pg) {
+    EntryPlan p{};
+    p.ae = ae;
+    p.s = s0;
+    p.m = m;
+    p.pad = pad;
+    p.ps = final ? 0u : m;
+    return chunk_desc(p, c, seed, entry, slot, pg);
+}
+
+// Writes every chunk descriptor. Heads go to their step bin (LDS atomic cursor per bin); the full
+// chunks of the block's entries form one contiguous run in the full bin, written by the whole
+// block (one descriptor per thread per pass, coalesced, no per-entry serial loop) — including
+// entries with thousands of chunks.
 __global__ void __launch_bounds__(kPlanBlock) plan_emit_kernel(const uint64_t* __restrict__ offsets,
                                                                const uint32_t* __restrict__ lengths,
                                                                const uint32_t* __restrict__ seeds, uint32_t seed_all,
                                                                uint64_t size, uint64_t n, PlanGeo pg,
                                                                uint64_t capacity, const uint32_t* __restrict__ blkoff,
-                                                               uint32_t* __restrict__ pslot,
-                                                               uint32_t* __restrict__ run_start,
-                                                               uint32_t* __restrict__ big, uint32_t* __restrict__ hdr,
+                                                               uint32_t* __restrict__ pslot, uint32_t* __restrict__ hdr,
                                                                PlanDesc* __restrict__ descs) {
     __shared__ uint32_t wsum[kPlanBlock / 64 + 1];
     __shared__ uint32_t cursor[kMaxJC + 2];
+    __shared__ uint32_t exf[kPlanBlock + 1];  // block-exclusive scan of full-chunk counts (+ total)
+    __shared__ int64_t st_ae[kPlanBlock], st_s[kPlanBlock];
+    __shared__ uint32_t st_m[kPlanBlock], st_flags[kPlanBlock], st_seed[kPlanBlock], st_slot[kPlanBlock];
     const uint32_t ncols = plan_ncols(pg);
     for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) cursor[k] = hdr[kHdrBase + k];
     __syncthreads();
@@ -254,36 +273,51 @@ __global__ void __launch_bounds__(kPlanBlock) plan_emit_kernel(const uint64_t* _
     uint32_t t_full, t_ps;
     const uint32_t ex_full = block_excl_scan(chunked ? p.full : 0u, wsum, t_full);
     const uint32_t ex_ps = block_excl_scan(chunked ? p.ps : 0u, wsum, t_ps);
-    if (i >= n) return;
-    if (!chunked) {
-        pslot[i] = kSerial;
-        return;
+    const uint32_t run0 = cursor[pg.jc];  // the block's first full-bin position (heads never move it)
+    exf[threadIdx.x] = ex_full;
+    if (threadIdx.x == 0) exf[kPlanBlock] = t_full;
+    if (i < n && !chunked) pslot[i] = kSerial;
+    if (chunked) {
+        const uint32_t rs = run0 + ex_full;
+        const uint32_t sb = cursor[slot_col(pg)] + ex_ps;
+        const bool has_head = p.jh != pg.jc;
+        const uint32_t hpos = has_head ? atomicAdd(&cursor[p.jh], 1u) : 0u;
+        const bool overflow = ((uint64_t)rs + p.full > capacity) || (has_head && (uint64_t)hpos >= capacity) ||
+                              (p.ps && (uint64_t)sb + p.ps > capacity);
+        pslot[i] = overflow ? kDirect : (p.ps ? sb : kNoSlot);
+        const uint32_t seed = seeds ? seeds[i] : seed_all;
+        if (has_head && (uint64_t)hpos < capacity)
+            descs[hpos] = overflow ? skip_desc() : chunk_desc(p, p.m - 1u, seed, (uint32_t)i, sb, pg);
+        st_ae[threadIdx.x] = p.ae;
+        st_s[threadIdx.x] = p.s;
+        st_m[threadIdx.x] = p.m;
+        st_flags[threadIdx.x] = p.pad | (p.ps == 0u ? 0x100u : 0u) | (overflow ? 0x200u : 0u);
+        st_seed[threadIdx.x] = seed;
+        st_slot[threadIdx.x] = sb;
     }
-    const uint32_t rs = cursor[pg.jc] + ex_full;
-    const uint32_t sb = cursor[slot_col(pg)] + ex_ps;
-    const bool has_head = p.jh != pg.jc;
-    const uint32_t hpos = has_head ? atomicAdd(&cursor[p.jh], 1u) : 0u;
-    const bool overflow = ((uint64_t)rs + p.full > capacity) || (has_head && (uint64_t)hpos >= capacity) ||
-                          (p.ps && (uint64_t)sb + p.ps > capacity);
-    run_start[i] = rs;
-    if (overflow) {
-        pslot[i] = kDirect;
-        for (uint32_t c = 0; c < p.full && (uint64_t)rs + c < capacity; ++c) descs[rs + c] = skip_desc();
-        if (has_head && (uint64_t)hpos < capacity) descs[hpos] = skip_desc();
-        return;
-    }
-    pslot[i] = p.ps ? sb : kNoSlot;
-    const uint32_t seed = seeds ? seeds[i] : seed_all;
-    if (has_head) descs[hpos] = chunk_desc(p, p.m - 1u, seed, (uint32_t)i, sb, pg);
-    if (p.full <= kEmitMax) {
-        for (uint32_t c = 0; c < p.full; ++c) descs[rs + c] = chunk_desc(p, c, seed, (uint32_t)i, sb, pg);
-    } else {
-        big[atomicAdd(&hdr[kHdrBig], 1u)] = (uint32_t)i;
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < t_full; k += kPlanBlock) {
+        // owner: the last thread t with exf[t] <= k (it has full chunks: exf[t + 1] > k)
+        uint32_t lo = 0u, hi = kPlanBlock;
+        while (hi - lo > 1u) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (exf[mid] <= k) lo = mid;
+            else hi = mid;
+        }
+        const uint32_t t = lo, c = k - exf[t];
+        const uint64_t pos = (uint64_t)run0 + k;
+        const uint32_t fl = st_flags[t];
+        if (fl & 0x200u) {
+            if (pos < capacity) descs[pos] = skip_desc();
+        } else {
+            descs[pos] = chunk_desc_of(st_ae[t], st_s[t], st_m[t], fl & 0xFFu, (fl & 0x100u) != 0u, c, st_seed[t],
+                                       (uint32_t)((uint64_t)blockIdx.x * kPlanBlock + t), st_slot[t], pg);
+        }
     }
 }
 
-// Entries the plan could not hold (pslot == kDirect): one entry per lane group, like IndexedSrc.
-// count() is 0 unless the plan overflowed (total chunks > capacity), so the pass is free otherwise.
+// Entries the plan could not hold (pslot == kDirect): one entry per lane group, like IndexedSrc,
+// in the chunk kernel's tail. count() is 0 unless the plan overflowed (total chunks > capacity).
 struct PlanDirectSrc {
     uint64_t n;
     const uint64_t* offsets;
@@ -306,23 +340,6 @@ struct PlanDirectSrc {
         return 0;
     }
 };
-
-// Full-bucket descriptors of entries with more than kEmitMax chunks: one block per entry.
-__global__ void plan_expand_big_kernel(const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ lengths,
-                                       const uint32_t* __restrict__ seeds, uint32_t seed_all, uint64_t size, PlanGeo pg,
-                                       const uint32_t* __restrict__ pslot, const uint32_t* __restrict__ run_start,
-                                       const uint32_t* __restrict__ big, const uint32_t* __restrict__ hdr,
-                                       PlanDesc* __restrict__ descs) {
-    const uint32_t nbig = hdr[kHdrBig];
-    for (uint32_t k = blockIdx.x; k < nbig; k += gridDim.x) {
-        const uint32_t i = big[k];
-        const EntryPlan p = plan_entry(offsets[i], lengths[i], size, pg);
-        const uint32_t seed = seeds ? seeds[i] : seed_all;
-        const uint32_t rs = run_start[i], sb = pslot[i];
-        for (uint32_t c = threadIdx.x; c < p.full; c += blockDim.x)
-            descs[rs + c] = chunk_desc(p, c, seed, i, sb, pg);
-    }
-}
 
 // a * b mod P, bitwise (no tables): 32 shift/xor steps, for the few products per entry that have
 // no operator table (x^(-8*pad), powers of X).
@@ -347,86 +364,86 @@ __device__ __forceinline__ uint32_t gf_pow_bits(uint32_t x, uint32_t e, uint32_t
 }
 
 // Horner over the partial registers of each chunked entry, then x^(-8*pad); serial fold of
-// entries the plan did not chunk. Entries with more than kEmitMax full chunks (the big list) are
-// left to plan_combine_big_kernel.
-__global__ void plan_combine_kernel(const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets,
-                                    const uint32_t* __restrict__ lengths, const uint32_t* __restrict__ seeds,
-                                    uint32_t seed_all, uint64_t size, uint64_t n, PlanGeo pg,
-                                    const uint32_t* __restrict__ xtab, const uint32_t* __restrict__ x32tab,
-                                    const uint32_t* __restrict__ btab, const uint32_t* __restrict__ xinv,
-                                    uint32_t poly, const uint32_t* __restrict__ pslot, const uint32_t* __restrict__ partials,
-                                    uint32_t* __restrict__ out, uint32_t* __restrict__ err) {
+// entries the plan did not chunk. Entries with more than kCombineSerial chunks (e.g. one 64 MiB
+// entry = 16 Ki chunks) are combined by the whole block instead of one serial thread: thread t
+// folds its contiguous run of partials with Horner (table X in LDS), is placed by X^(first chunk
+// of its run) (bitwise power), and the block XOR-reduces.
+constexpr uint32_t kCombineSerial = 64;
+
+__device__ __forceinline__ uint32_t mul_x(const uint32_t* X, uint32_t r) {
+    return X[r & 0xffu] ^ X[256 + ((r >> 8) & 0xffu)] ^ X[512 + ((r >> 16) & 0xffu)] ^ X[768 + (r >> 24)];
+}
+
+__global__ void __launch_bounds__(1024) plan_combine_kernel(
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ lengths,
+    const uint32_t* __restrict__ seeds, uint32_t seed_all, uint64_t size, uint64_t n, PlanGeo pg,
+    const uint32_t* __restrict__ xtab, uint32_t xval, const uint32_t* __restrict__ x32tab,
+    const uint32_t* __restrict__ btab, const uint32_t* __restrict__ xinv, uint32_t poly,
+    const uint32_t* __restrict__ pslot, const uint32_t* __restrict__ partials, uint32_t* __restrict__ out,
+    uint32_t* __restrict__ err) {
     __shared__ uint32_t X[1024];
     __shared__ uint32_t W[1024];
     __shared__ uint32_t B[256];
+    __shared__ uint32_t big[1024];
+    __shared__ uint32_t nbig;
+    __shared__ uint32_t red[1024 / 64];
     for (int k = threadIdx.x; k < 1024; k += blockDim.x) X[k] = xtab[k];
     for (int k = threadIdx.x; k < 1024; k += blockDim.x) W[k] = x32tab[k];
     for (int k = threadIdx.x; k < 256; k += blockDim.x) B[k] = btab[k];
+    if (threadIdx.x == 0) nbig = 0u;
     __syncthreads();
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t slot = pslot[i];
-    if (slot == kNoSlot) return;
-    const uint64_t o = offsets[i];
-    const uint32_t l = lengths[i];
-    if (!entry_valid(o, l, size)) {
-        out[i] = 0u;
-        if (err) atomicOr(err, 1u);
-        return;
-    }
-    if (slot == kDirect) return;  // the overflow pass (PlanDirectSrc) computes it
-    if (slot == kSerial) {
-        uint32_t reg = ~(seeds ? seeds[i] : seed_all);
-        const uint8_t* q = base + o;
-        const uint8_t* qe = q + l;
-        // bytes up to a 4-byte boundary, aligned dwords by x^32, trailing bytes
-        while (q < qe && ((uintptr_t)q & 3u)) reg = B[(reg ^ *q++) & 0xffu] ^ (reg >> 8);
-        for (; qe - q >= 4; q += 4) {
-            const uint32_t r = reg ^ *reinterpret_cast<const uint32_t*>(q);
-            reg = W[r & 0xffu] ^ W[256 + ((r >> 8) & 0xffu)] ^ W[512 + ((r >> 16) & 0xffu)] ^ W[768 + (r >> 24)];
+    const uint32_t slot = i < n ? pslot[i] : kNoSlot;
+    if (slot != kNoSlot && slot != kDirect) {
+        const uint64_t o = offsets[i];
+        const uint32_t l = lengths[i];
+        if (!entry_valid(o, l, size)) {
+            out[i] = 0u;
+            if (err) atomicOr(err, 1u);
+        } else if (slot == kSerial) {
+            uint32_t reg = ~(seeds ? seeds[i] : seed_all);
+            const uint8_t* q = base + o;
+            const uint8_t* qe = q + l;
+            // bytes up to a 4-byte boundary, aligned dwords by x^32, trailing bytes
+            while (q < qe && ((uintptr_t)q & 3u)) reg = B[(reg ^ *q++) & 0xffu] ^ (reg >> 8);
+            for (; qe - q >= 4; q += 4) {
+                const uint32_t r = reg ^ *reinterpret_cast<const uint32_t*>(q);
+                reg = W[r & 0xffu] ^ W[256 + ((r >> 8) & 0xffu)] ^ W[512 + ((r >> 16) & 0xffu)] ^ W[768 + (r >> 24)];
+            }
+            while (q < qe) reg = B[(reg ^ *q++) & 0xffu] ^ (reg >> 8);
+            out[i] = ~reg;
+        } else {
+            const EntryPlan p = plan_entry(o, l, size, pg);
+            if (p.m > kCombineSerial) {
+                big[atomicAdd(&nbig, 1u)] = (uint32_t)threadIdx.x;
+            } else {
+                // partials in batches of 8 independent loads, then Horner from the head
+                uint32_t reg = partials[slot + p.m - 1u];
+                for (int c0 = (int)p.m - 2; c0 >= 0; c0 -= 8) {
+                    uint32_t pv[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) pv[k] = c0 - k >= 0 ? partials[slot + (uint32_t)(c0 - k)] : 0u;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                        if (c0 - k >= 0) reg = mul_x(X, reg) ^ pv[k];
+                }
+                // undo the zero padding: reg * x^(-8*pad), a bitwise product (no table dependency chain)
+                if (p.pad) reg = gf_mul_bits(xinv[p.pad], reg, poly);
+                out[i] = ~reg;
+            }
         }
-        while (q < qe) reg = B[(reg ^ *q++) & 0xffu] ^ (reg >> 8);
-        out[i] = ~reg;
-        return;
     }
-    const EntryPlan p = plan_entry(o, l, size, pg);
-    if (p.full > kEmitMax) return;
-    uint32_t reg = partials[slot + p.m - 1u];
-    for (int c = (int)p.m - 2; c >= 0; --c) {
-        reg = X[reg & 0xffu] ^ X[256 + ((reg >> 8) & 0xffu)] ^ X[512 + ((reg >> 16) & 0xffu)] ^ X[768 + (reg >> 24)];
-        reg ^= partials[slot + (uint32_t)c];
-    }
-    // undo the zero padding: reg * x^(-8*pad), a bitwise product (no table dependency chain)
-    if (p.pad) reg = gf_mul_bits(xinv[p.pad], reg, poly);
-    out[i] = ~reg;
-}
-
-// Combine of the big-list entries (> kEmitMax chunks, e.g. one 64 MiB entry = 16 Ki chunks): one
-// block per entry instead of one serial Horner thread. Thread t folds its contiguous run of
-// partials with Horner (table X in LDS), is placed by X^(first chunk of its run) (bitwise power),
-// and the block XOR-reduces: reg = sum_c partial_c * X^c, then * x^(-8*pad) as in plan_combine.
-__global__ void __launch_bounds__(256) plan_combine_big_kernel(
-    const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ lengths, uint64_t size, PlanGeo pg,
-    const uint32_t* __restrict__ xtab, uint32_t xval, const uint32_t* __restrict__ xinv, uint32_t poly,
-    const uint32_t* __restrict__ pslot, const uint32_t* __restrict__ partials, const uint32_t* __restrict__ big,
-    const uint32_t* __restrict__ hdr, uint32_t* __restrict__ out) {
-    __shared__ uint32_t X[1024];
-    __shared__ uint32_t red[256 / 64];
-    for (int k = threadIdx.x; k < 1024; k += blockDim.x) X[k] = xtab[k];
     __syncthreads();
-    const uint32_t nbig = hdr[kHdrBig];
-    for (uint32_t k = blockIdx.x; k < nbig; k += gridDim.x) {
-        const uint32_t i = big[k];
-        const uint32_t slot = pslot[i];
-        const EntryPlan p = plan_entry(offsets[i], lengths[i], size, pg);
+    const uint32_t nb = nbig;
+    for (uint32_t k = 0; k < nb; ++k) {
+        const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + big[k];
+        const uint32_t sl = pslot[e];
+        const EntryPlan p = plan_entry(offsets[e], lengths[e], size, pg);
         const uint32_t per = (p.m + blockDim.x - 1u) / blockDim.x;
         const uint32_t lo = threadIdx.x * per;
         const uint32_t hi = lo + per < p.m ? lo + per : p.m;
         uint32_t r = 0u;
-        for (int c = (int)hi - 1; c >= (int)lo; --c) {
-            r = X[r & 0xffu] ^ X[256 + ((r >> 8) & 0xffu)] ^ X[512 + ((r >> 16) & 0xffu)] ^ X[768 + (r >> 24)];
-            r ^= partials[slot + (uint32_t)c];
-        }
+        for (int c = (int)hi - 1; c >= (int)lo; --c) r = mul_x(X, r) ^ partials[sl + (uint32_t)c];
         if (lo < hi && lo) r = gf_mul_bits(gf_pow_bits(xval, lo, poly), r, poly);
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) r ^= (uint32_t)__shfl_xor((int)r, d);
@@ -436,7 +453,7 @@ __global__ void __launch_bounds__(256) plan_combine_big_kernel(
             uint32_t reg = 0u;
             for (uint32_t w = 0; w < blockDim.x / 64; ++w) reg ^= red[w];
             if (p.pad) reg = gf_mul_bits(xinv[p.pad], reg, poly);
-            out[i] = ~reg;
+            out[e] = ~reg;
         }
         __syncthreads();
     }

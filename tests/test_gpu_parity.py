@@ -291,7 +291,7 @@ def test_digest_batch_package_and_verify(gpu, dtype, algo):
 
 def test_plan_overflow_falls_back_to_direct(gpu):
     """Heavily overlapping entries exceed the plan's capacity (n + size/CH + 16 chunks); the
-    overflowing entries are computed by the combine kernel's serial fallback, still bit-exact."""
+    overflowing entries are computed one entry per group in the chunk kernel's tail, bit-exact."""
     import torch
     ck.set_plan_mode(2)
     size = 1 << 20

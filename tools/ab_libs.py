@@ -1,0 +1,98 @@
+"""A/B several builds of libbkdigest.so in ONE process on the same device buffers, interleaved
+rounds (cdna_hip_programming.md §5.4 rule 24: cross-box and first-run noise is larger than the
+effects being measured).
+
+Usage (GPU box): python3 tools/ab_libs.py [lib.so ...]
+Default libraries: bookkeeper_amd/libbkdigest.so and every tools/variants/lib_*.so.
+Workloads: zipf (config 3), zipf crc32, zipf < 1 KiB bucket, packed 64 B, indexed 4 KiB, uniform 4 KiB.
+Each library's digests must equal the first library's, bit for bit.
+"""
+import ctypes
+import glob
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+ROUNDS = int(os.environ.get("AB_ROUNDS", "5"))
+REPS = 10
+
+
+def main(paths):
+    import numpy as np
+    import torch
+    from bench import zipf_index
+    from bookkeeper_amd import _native
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    st = torch.cuda.current_stream()
+    libs = {}
+    for p in paths:
+        L = ctypes.CDLL(os.path.abspath(p))
+        for fn, (res, args) in _native.PROTOTYPES.items():
+            if hasattr(L, fn):
+                getattr(L, fn).restype = res
+                getattr(L, fn).argtypes = args
+        libs[os.path.basename(p)] = L
+    n = 1 << 20
+    offs, lens = zipf_index(n)
+    total = int(offs[-1] + lens[-1])
+    base = torch.empty(max(total, n * 4096), dtype=torch.uint8, device=dev)
+    first = next(iter(libs.values()))
+    first.bkd_fill_splitmix64(ctypes.c_void_p(base.data_ptr()), base.numel(), 42, 0, None)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    ptr = lambda t: ctypes.c_void_p(t.data_ptr())
+
+    def idx(o, l):
+        return (torch.from_numpy(np.ascontiguousarray(o, dtype=np.int64)).to(dev),
+                torch.from_numpy(np.ascontiguousarray(l).astype(np.int32)).to(dev))
+
+    lt = lens < 1024
+    work = {
+        "zipf": (0, *idx(offs, lens), total),
+        "zipf_crc32": (1, *idx(offs, lens), total),
+        "zipf_lt1k": (0, *idx(offs[lt], lens[lt]), int(lens[lt].sum())),
+        "packed64": (0, *idx(np.arange(n) * 64, np.full(n, 64)), n * 64),
+        "indexed4k": (0, *idx(np.arange(n) * 4096, np.full(n, 4096)), n * 4096),
+    }
+
+    def call(L, name):
+        if name == "uniform4k":
+            return L.bkd_crc_batch_uniform(0, ptr(base), 4096, 4096, n, None, 0, ptr(out), ctypes.c_void_p(st.cuda_stream))
+        algo, o, l, _ = work[name]
+        return L.bkd_crc_batch(algo, ptr(base), base.numel(), ptr(o), ptr(l), o.numel(), None, 0, ptr(out),
+                               ctypes.c_void_p(st.cuda_stream))
+
+    names = list(work) + ["uniform4k"]
+    res = {}
+    for name in names:
+        ref = None
+        for L in libs.values():  # warm-up + parity
+            L.bkd_set_plan_mode(0)
+            assert call(L, name) == 0, name
+            torch.cuda.synchronize()
+            cnt = work[name][1].numel() if name in work else n
+            if ref is None:
+                ref = out[:cnt].clone()
+            assert torch.equal(out[:cnt], ref), f"{name}: digests differ between libraries"
+        for _ in range(ROUNDS):
+            for lname, L in libs.items():
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                for _ in range(REPS):
+                    call(L, name)
+                e1.record(st)
+                torch.cuda.synchronize()
+                res.setdefault((name, lname), []).append(e0.elapsed_time(e1) / REPS)
+        nbytes = work[name][3] if name in work else n * 4096
+        for lname in libs:
+            v = sorted(res[(name, lname)])
+            print(f"{name:12s} {lname:22s} median {v[len(v) // 2]:.4f} ms  min {v[0]:.4f} ms  "
+                  f"{nbytes / v[len(v) // 2] / 1e6:7.0f} GB/s payload", flush=True)
+
+
+if __name__ == "__main__":
+    args = sys.argv[1:] or [os.path.join(ROOT, "bookkeeper_amd", "libbkdigest.so")] + sorted(
+        glob.glob(os.path.join(ROOT, "tools", "variants", "lib_*.so")))
+    main(args)
