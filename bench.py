@@ -116,6 +116,49 @@ def cpu_baseline(host_sample: np.ndarray, entry_len: int, algo: int = 0, budget_
                       f"{reps} passes over {cores} std::threads, one call per entry; {label}"}, out
 
 
+def cpu_baseline_indexed(host: np.ndarray, offs: np.ndarray, lens: np.ndarray, algo: int = 0, budget_s: float = 8.0):
+    """Config 3's CPU leg: one CRC per entry of an offset+length sample on the host cores. CRC32C:
+    the reference's own circe crc32c() (oracle/_ref); CRC32: zlib's crc32(), the arithmetic
+    java.util.zip.CRC32 runs (CRC32DigestManager.java:28-87)."""
+    import oracle
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        cores = os.cpu_count() or 1
+    cores = max(1, min(16, cores))
+    n = offs.size
+    out = np.zeros(n, dtype=np.uint32)
+    o64 = np.ascontiguousarray(offs, dtype=np.uint64)
+    l32 = np.ascontiguousarray(lens, dtype=np.uint32)
+    ref = oracle.ref()
+    if algo == 0 and ref is not None:
+        kind, label = "reference", "circe crc32c() compiled from /root/reference"
+        u8p = host.ctypes.data_as(oracle._u8p)
+
+        def run(thr, reps):
+            return ref.ref_crc32c_batch_timed(u8p, o64.ctypes.data_as(oracle._u64p), l32.ctypes.data_as(oracle._u32p),
+                                              n, thr, reps, out.ctypes.data_as(oracle._u32p))
+    else:
+        kind = "port"
+        label = ("zlib crc32() (the arithmetic of java.util.zip.CRC32, whose JDK intrinsic is PCLMUL-based and "
+                 "faster than this zlib 1.2.11 table loop), oracle/cpu_baseline.c")
+        lib = oracle.lib()
+        u8p = host.ctypes.data_as(oracle._u8p)
+
+        def run(thr, reps):
+            return lib.oracle_zlib_crc32_batch_timed(u8p, o64.ctypes.data_as(oracle._u64p),
+                                                     l32.ctypes.data_as(oracle._u32p), n, thr, reps,
+                                                     out.ctypes.data_as(oracle._u32p))
+    nbytes = int(l32.sum())
+    t1 = run(1, 1)
+    reps = max(1, int(budget_s / max(1e-6, t1 / cores)))
+    t = run(cores, reps)
+    return {"value": round(nbytes * reps / t / GIB, 3), "unit": "GiB/s", "cores": cores, "kind": kind,
+            "single_core_value": round(nbytes / t1 / GIB, 3), "cpu_model": _cpu_model(),
+            "sample": f"the first {n} entries of the same Zipf index ({nbytes / GIB:.3f} GiB), {reps} passes over "
+                      f"{cores} threads, one call per entry; {label}"}, out
+
+
 def _cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -183,12 +226,77 @@ def host_bench(args, ck, torch, rank) -> None:
         print(json.dumps(res), flush=True)
 
 
+def digest_bench(args, ck, torch, rank, dev, stream, algo) -> None:
+    """SURVEY §8f rows 1-2 (not the headline): framed ledger entries [32 B header][digest][payload]
+    of 4 KiB each, device-resident. Times DigestManager's batched verify (BatchedReadOp's loop,
+    BatchedReadOp.java:164-190 -> bkd_digest_verify_batch) and batched packaging (PendingAddOp /
+    LedgerFragmentReplicator -> bkd_digest_package_batch) over the same n entries."""
+    from bookkeeper_amd import digest as dg
+    n = args.entries or (1 << 20)
+    L = 4096
+    dm = dg.DigestManager.instantiate(7, b"", dg.DigestType.CRC32C if algo == ck.CRC32C else dg.DigestType.CRC32)
+    mac = dm.macCodeLength
+    framed = torch.empty(n * L, dtype=torch.uint8, device=dev)
+    ck.fill_splitmix64(framed, 42)
+    ids = torch.arange(n, dtype=torch.int64, device=dev)
+    lacs = ids - 1
+    plen = L - 32 - mac
+    pay_off = ids * L + 32 + mac
+    pay_len = torch.full((n,), plen, dtype=torch.int32, device=dev)
+    len_field = torch.full((n,), plen, dtype=torch.int64, device=dev)
+    frames, digests = dm.package_batch(ids, lacs, len_field, framed, pay_off, pay_len, stream=stream)
+    framed.view(n, L)[:, :32 + mac].copy_(frames)
+    f_off = ids * L
+    f_len = torch.full((n,), L, dtype=torch.int32, device=dev)
+
+    def timed(fn):
+        for _ in range(max(1, args.warmup)):
+            fn()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(args.steps):
+            fn()
+        b.record(stream)
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / 1e3 / args.steps
+
+    t_verify = timed(lambda: dm.verify_batch(framed, f_off, f_len, 0, stream=stream))
+    status, first_bad = dm.verify_batch(framed, f_off, f_len, 0, stream=stream)
+    torch.cuda.synchronize()
+    ok = bool((status == 0).all().item()) and int(first_bad.item()) == n
+    t_pack = timed(lambda: dm.package_batch(ids, lacs, len_field, framed, pay_off, pay_len, stream=stream))
+    # algorithmic bytes: verify reads every framed byte + 12 B of index, writes a 4 B status;
+    # package reads the payload + 24 B of ids/LAC/length + 12 B of index, writes header+digest + 4 B
+    v_bytes = n * (L + 12 + 4)
+    p_bytes = n * (plen + 24 + 12 + 32 + mac + 4)
+    res = {"metric": "GiB/s framed 4 KiB ledger entries, batched DigestManager verify (BatchedReadOp), "
+                     "device-resident (not the headline)",
+           "value": round(n * L / t_verify / GIB, 2), "unit": "GiB/s", "n_gpus": 1, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(t_verify * 1e3, 4), "higher_is_better": True,
+           "dtype": "u8", "data": "synthetic (device-generated splitmix64, seed 42, framed by package_batch)",
+           "config": {"workload": f"{n} framed entries x {L} B ({args.algo}: 32 B header + {mac} B digest + "
+                                  f"{plen} B payload), verify = header CRC -> payload CRC -> compare"},
+           "all_verified": ok,
+           "roofline": {"bound": "hbm", "achieved": round(v_bytes / t_verify / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(v_bytes / t_verify / 1e9 / HBM_PEAK_GBS, 4),
+                        "traffic": None, "kernel": "verify pipeline (verify_header + plan/chunks + verify_finish)",
+                        "algorithmic_bytes_per_launch": v_bytes},
+           "package": {"GiB_s_payload": round(n * plen / t_pack / GIB, 2), "ms": round(t_pack * 1e3, 4),
+                       "achieved_GB_s": round(p_bytes / t_pack / 1e9, 1),
+                       "algorithmic_bytes_per_launch": p_bytes}}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if not ok:
+        raise SystemExit("VERIFY FAILURE: freshly packaged entries did not verify")
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--config", default="uniform4k", choices=["uniform4k", "shard8m", "zipf", "indexed4k", "host4k"])
+    ap.add_argument("--config", default="uniform4k", choices=["uniform4k", "shard8m", "zipf", "indexed4k", "host4k", "verify4k"])
     ap.add_argument("--algo", default="crc32c", choices=["crc32c", "crc32"])
     ap.add_argument("--entries", type=int, default=0, help="entries per GPU (default by config)")
     ap.add_argument("--lanes", type=int, default=0, help="force lanes per entry group (0 = auto)")
@@ -230,6 +338,8 @@ def main() -> None:
     stream = torch.cuda.current_stream(dev)
     if args.config == "host4k":
         return host_bench(args, ck, torch, rank)
+    if args.config == "verify4k":
+        return digest_bench(args, ck, torch, rank, dev, stream, algo)
     if args.config in ("uniform4k", "shard8m"):
         entry_len = 4096
         n = args.entries or (1 << 20 if args.config == "uniform4k" else 8 << 20)
@@ -319,6 +429,16 @@ def main() -> None:
     }
     if args.config == "zipf" and world == 1 and not args.no_buckets:
         result["buckets"] = bucket_rates(ck, torch, algo, base, offs, lens, stream, max(3, args.steps))
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "zipf":
+        m = min(n, 65536)  # ~0.4 GiB of the same packed buffer
+        span = int(offs[m - 1] + lens[m - 1])
+        host = np.ascontiguousarray(base[:span].cpu().numpy())
+        result["cpu_baseline"], want = cpu_baseline_indexed(host, offs[:m], lens[:m], algo)
+        got = out[:m].cpu().numpy().view(np.uint32)
+        result["parity_check"] = {"entries": m, "match": bool((got == want).all())}
+        if not result["parity_check"]["match"]:
+            print(json.dumps(result), flush=True)
+            raise SystemExit("PARITY FAILURE: GPU digests differ from the CPU baseline's")
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in ("uniform4k", "shard8m"):
         # cpu_baseline leg: the reference timed on the host cores over a bounded sample; its
         # digests for that sample double as a parity spot check of the GPU output.

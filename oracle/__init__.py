@@ -87,6 +87,9 @@ def lib():
         L.oracle_entrylog_scan.restype = ctypes.c_uint64
         L.oracle_entrylog_scan.argtypes = [_u8p, ctypes.c_uint64, ctypes.c_uint64, _u64p, _u32p,
                                            ctypes.POINTER(ctypes.c_int64), ctypes.c_uint64, _u64p]
+        L.oracle_zlib_crc32_batch_timed.restype = ctypes.c_double
+        L.oracle_zlib_crc32_batch_timed.argtypes = [_u8p, _u64p, _u32p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                                    _u32p]
         L.oracle_table.restype = None
         L.oracle_table.argtypes = [ctypes.c_int, _u32p]
         _lib = L
@@ -112,6 +115,8 @@ def ref():
         L.ref_crc32c_uniform_timed.restype = ctypes.c_double
         L.ref_crc32c_uniform_timed.argtypes = [_u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
                                                ctypes.c_int, ctypes.c_int, _u32p]
+        L.ref_crc32c_batch_timed.restype = ctypes.c_double
+        L.ref_crc32c_batch_timed.argtypes = [_u8p, _u64p, _u32p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, _u32p]
         _ref = L
     return _ref
 

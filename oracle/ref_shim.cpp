@@ -75,4 +75,36 @@ double ref_crc32c_uniform_timed(const uint8_t* base, uint64_t stride, uint32_t l
     return std::chrono::duration<double>(t1 - t0).count();
 }
 
+// Times `reps` passes of one crc32c() call per indexed entry (an offset+length batch, e.g. the
+// Zipf config), entries split into contiguous ranges of about equal bytes over `threads`.
+double ref_crc32c_batch_timed(const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths, uint64_t n,
+                              int threads, int reps, uint32_t* out) {
+    crc32c_initialize();
+    const chunk_config* cfg = &default_config();
+    if (threads < 1) threads = 1;
+    std::vector<uint64_t> cut(threads + 1, n);
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; ++i) total += lengths[i];
+    cut[0] = 0;
+    uint64_t acc = 0;
+    int t = 1;
+    for (uint64_t i = 0; i < n && t < threads; ++i) {
+        acc += lengths[i];
+        while (t < threads && acc * threads >= total * t) cut[t++] = i + 1;
+    }
+    auto t0 = std::chrono::steady_clock::now();
+    for (int r = 0; r < reps; ++r) {
+        std::vector<std::thread> pool;
+        for (int k = 0; k < threads; ++k) {
+            const uint64_t lo = cut[k], hi = cut[k + 1];
+            pool.emplace_back([=]() {
+                for (uint64_t i = lo; i < hi; ++i) out[i] = crc32c(0, base + offsets[i], lengths[i], cfg);
+            });
+        }
+        for (auto& th : pool) th.join();
+    }
+    auto t1 = std::chrono::steady_clock::now();
+    return std::chrono::duration<double>(t1 - t0).count();
+}
+
 }  // extern "C"
