@@ -27,7 +27,7 @@ from . import _native
 from ._native import CRC32, CRC32C, check, lib
 
 __all__ = ["CRC32C", "CRC32", "GpuIntHash", "Crc32cIntChecksum", "crc_batch", "crc_batch_uniform",
-           "crc_batch_host", "to_java_int"]
+           "crc_batch_segments", "crc_batch_host", "to_java_int"]
 
 
 def to_java_int(v: int) -> int:
@@ -182,6 +182,32 @@ def crc_batch(algo: int, base, offsets, lengths, seeds=None, seed_all: int = 0, 
     check(lib().bkd_crc_batch(algo, _dev_ptr(base, "base"), nbytes, _dev_ptr(offsets, "offsets", torch.int64),
                               _dev_ptr(lengths, "lengths", torch.int32), n, _dev_ptr(seeds, "seeds"),
                               seed_all & 0xFFFFFFFF, _dev_ptr(out, "out"), st))
+    if sync_check:
+        check(lib().bkd_stream_sync(st))
+    return out
+
+
+def crc_batch_segments(algo: int, base, seg_offsets, seg_lengths, seg_first, seeds=None, seed_all: int = 0,
+                       out=None, stream=None, sync_check: bool = False):
+    """Composite entries (bkd_crc_batch_segments): out[i] = resume(seed_i, the concatenation of
+    segments seg_first[i] .. seg_first[i+1]-1), segment k = base[seg_offsets[k] : + seg_lengths[k]].
+
+    seg_offsets: int64, seg_lengths: int32, seg_first: int64 with n + 1 entries (torch, on the device)."""
+    import torch
+    nseg = seg_offsets.numel()
+    n = seg_first.numel() - 1
+    if n < 0:
+        raise ValueError("seg_first needs n + 1 entries")
+    if seg_lengths.numel() != nseg:
+        raise ValueError("seg_offsets/seg_lengths size mismatch")
+    if out is None:
+        out = torch.empty(max(n, 0), dtype=torch.int32, device=base.device)
+    st = _stream_ptr(stream, base)
+    check(lib().bkd_crc_batch_segments(algo, _dev_ptr(base, "base"), base.numel() * base.element_size(),
+                                       _dev_ptr(seg_offsets, "seg_offsets", torch.int64),
+                                       _dev_ptr(seg_lengths, "seg_lengths", torch.int32), nseg,
+                                       _dev_ptr(seg_first, "seg_first", torch.int64), n, _dev_ptr(seeds, "seeds"),
+                                       seed_all & 0xFFFFFFFF, _dev_ptr(out, "out"), st))
     if sync_check:
         check(lib().bkd_stream_sync(st))
     return out

@@ -51,8 +51,8 @@ int lane_index(int lanes) {
 // hipFreeAsync left the GPU idle ~40 us between calls (profiles/r01_diag_ragged.log).
 struct StreamScratch {
     std::recursive_mutex mu;
-    uint8_t* buf[2] = {};  // slot 0: plan scratch (launch_plan), slot 1: verify pipeline
-    size_t cap[2] = {};
+    uint8_t* buf[3] = {};  // slot 0: plan scratch (launch_plan), 1: verify pipeline, 2: segment CRCs
+    size_t cap[3] = {};
     // Returns slot `which` with at least `bytes` bytes, stream-ordered on `st`.
     hipError_t get(int which, size_t bytes, hipStream_t st, uint8_t** out) {
         if (cap[which] < bytes) {
@@ -782,6 +782,39 @@ int bkd_entrylog_verify(int algo, const void* d_log, uint64_t log_size, const ui
                         const uint32_t* d_lengths, uint64_t n, int32_t* d_status, uint64_t* d_first_bad,
                         void* stream) {
     return verify_framed(algo, 0, 0, 2, d_log, log_size, d_offsets, d_lengths, n, d_status, d_first_bad, stream);
+}
+
+int bkd_crc_batch_segments(int algo, const void* d_base, uint64_t base_size, const uint64_t* d_seg_offsets,
+                           const uint32_t* d_seg_lengths, uint64_t nseg, const uint64_t* d_seg_first, uint64_t n,
+                           const uint32_t* d_seeds, uint32_t seed_all, uint32_t* d_out, void* stream) {
+    if (!valid_algo(algo)) return fail(BKD_ERR_INVALID_ARG, "unknown algorithm");
+    if (n == 0) return BKD_OK;
+    if (!d_seg_first || !d_out || (nseg && (!d_seg_offsets || !d_seg_lengths)))
+        return fail(BKD_ERR_INVALID_ARG, "null index/out");
+    if (nseg && !d_base && base_size) return fail(BKD_ERR_INVALID_ARG, "null base");
+    DeviceState* ds = nullptr;
+    int rc = ensure_current(&ds);
+    if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    StreamScratch& sc = scratch_for(*ds, st);
+    std::lock_guard<std::recursive_mutex> lk(sc.mu);  // held across the nested plan (slot 0)
+    uint8_t* seg = nullptr;
+    hipError_t e = sc.get(2, (size_t)std::max<uint64_t>(nseg, 1) * 4, st, &seg);
+    if (e != hipSuccess) return fail(BKD_ERR_NOMEM, std::string("segment scratch: ") + hipGetErrorString(e));
+    uint32_t* segcrc = reinterpret_cast<uint32_t*>(seg);
+    // every segment's raw register reg(0, segment), as ~resume(~0, segment)
+    if (nseg) {
+        rc = indexed_batch(*ds, algo, (const uint8_t*)d_base, base_size, d_seg_offsets, d_seg_lengths, nseg, nullptr,
+                           0xFFFFFFFFu, segcrc, st);
+        if (rc) return rc;
+    }
+    bkd::XPow8 pw;
+    for (int b = 0; b < 32; ++b) pw.p[b] = bkd::gf2::xpow(algo, 8ull << b);
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(bkd::segments_combine_kernel, dim3(blocks), dim3(256), 0, st, d_seg_lengths, segcrc,
+                       d_seg_first, n, d_seeds, seed_all, pw, bkd::gf2::poly(algo), d_out);
+    BKD_HIP(hipGetLastError());
+    return BKD_OK;
 }
 
 int bkd_entrylog_index(const void* h_log, uint64_t log_size, uint64_t start, uint64_t* h_offsets,

@@ -459,4 +459,33 @@ __global__ void __launch_bounds__(1024) plan_combine_kernel(
     }
 }
 
+// ---- composite entries (bkd_crc_batch_segments) ----
+// x^(8 * 2^b) mod P for b = 0..31: multiplying by x^(8*len) = one product per set bit of len.
+struct XPow8 {
+    uint32_t p[32];
+};
+
+// Entry i = segments first[i] .. first[i+1]-1 in order (DigestManager.update over ByteBufVisitor's
+// leaves, DigestManager.java:62-72,380-392): reg = ~seed; per non-empty segment k,
+// reg = reg * x^(8*len_k) ^ raw_k (raw_k = ~segcrc[k] = the segment's zero-initialised register);
+// out = ~reg. One thread per entry.
+__global__ void __launch_bounds__(256) segments_combine_kernel(const uint32_t* __restrict__ seg_lengths,
+                                                               const uint32_t* __restrict__ segcrc,
+                                                               const uint64_t* __restrict__ first, uint64_t n,
+                                                               const uint32_t* __restrict__ seeds, uint32_t seed_all,
+                                                               XPow8 pw, uint32_t poly, uint32_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t reg = ~(seeds ? seeds[i] : seed_all);
+    const uint64_t k1 = first[i + 1];
+    for (uint64_t k = first[i]; k < k1; ++k) {
+        uint32_t len = seg_lengths[k];
+        if (!len) continue;  // ByteBufVisitor skips empty buffers (ByteBufVisitor.java:100-103,146-149)
+        for (int b = 0; len; ++b, len >>= 1)
+            if (len & 1u) reg = gf_mul_bits(pw.p[b], reg, poly);
+        reg ^= ~segcrc[k];
+    }
+    out[i] = ~reg;
+}
+
 }  // namespace bkd

@@ -20,6 +20,7 @@ import struct
 import numpy as np
 
 from . import checksum as _ck
+from .bytebuf import CompositeBuffer
 from ._native import (CRC32, CRC32C, VERIFY_DIGEST_MISMATCH, VERIFY_ENTRY_MISMATCH, VERIFY_LEDGER_MISMATCH,
                       VERIFY_OK, VERIFY_TOO_SHORT, check, lib)
 
@@ -86,6 +87,15 @@ class DigestManager:
 
     # ---- the two hooks subclasses define (DigestManager.java:56-76) ----
     def update(self, digest: int, buf, offset: int, length: int) -> int:
+        """DigestManager.update (:62-72): a composite buffer is visited leaf by leaf and the digest
+        chained over the leaves (ByteBufVisitor, :380-392); anything else is one resume."""
+        if isinstance(buf, CompositeBuffer):
+            for leaf, off, n in buf.visit(offset, length):
+                digest = self.internalUpdate(digest, leaf, off, n)
+            return digest
+        return self.internalUpdate(digest, buf, offset, length)
+
+    def internalUpdate(self, digest: int, buf, offset: int, length: int) -> int:
         return self._hash.resume(digest, buf, offset, length)
 
     def digest_bytes(self, digest: int) -> bytes:
@@ -98,10 +108,14 @@ class DigestManager:
     def computeDigestAndPackageForSending(self, entryId: int, lastAddConfirmed: int, length: int, data: bytes,
                                           masterKey: bytes = b"\0" * MASTER_KEY_LENGTH,
                                           flags: int = FLAG_NONE) -> bytes:
-        data = bytes(data)
         hdr = _header(self.ledgerId, entryId, lastAddConfirmed, length)
         digest = self.update(0, hdr, 0, METADATA_LENGTH)
-        digest = self.update(digest, data, 0, len(data))
+        if isinstance(data, CompositeBuffer):  # the readable bytes, digested leaf by leaf (:152-153)
+            digest = self.update(digest, data, data.reader_index, data.readable_bytes())
+            data = data.readable()
+        else:
+            data = bytes(data)
+            digest = self.update(digest, data, 0, len(data))
         dbytes = self.digest_bytes(digest)
         if not self.useV2Protocol:  # V3: ByteBufList(header+digest, data)  (:169-181)
             return hdr + dbytes + data
@@ -213,7 +227,7 @@ class DummyDigestManager(DigestManager):
     algo = None
     macCodeLength = 0
 
-    def update(self, digest, buf, offset, length):
+    def internalUpdate(self, digest, buf, offset, length):
         return 0
 
     def digest_bytes(self, digest: int) -> bytes:

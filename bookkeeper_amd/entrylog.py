@@ -78,7 +78,7 @@ class EntryLogScrubber:
         if n == 0:
             return scan, status
         if log_device is None:
-            log_device = torch.from_numpy(np.ascontiguousarray(_ck._host_view(log_host))).cuda()
+            log_device = torch.from_numpy(np.array(_ck._host_view(log_host), copy=True)).cuda()
         dev = log_device.device
         types = np.array([self._ALGOS.get(self.digest_type_of(int(l)), -1) for l in scan.ledger_ids],
                          dtype=np.int32)

@@ -91,6 +91,18 @@ int bkd_crc_batch(int algo, const void* d_base, uint64_t base_size, const uint64
                   const uint32_t* d_lengths, uint64_t n, const uint32_t* d_seeds, uint32_t seed_all,
                   uint32_t* d_out, void* stream);
 
+/* Composite entries (a Netty CompositeByteBuf / ByteBufList visited leaf by leaf): entry i is the
+ * concatenation, in order, of segments d_seg_first[i] .. d_seg_first[i+1]-1, segment k being the
+ * byte range d_base + d_seg_offsets[k], d_seg_lengths[k] bytes; empty segments are skipped. out[i] =
+ * resume(seed_i, concatenation) — the digest DigestManager.update chains over ByteBufVisitor's
+ * leaves ($BK/proto/checksum/DigestManager.java:62-72,380-392, $BK/util/ByteBufVisitor.java:72-191),
+ * without copying the pieces together. d_seg_first holds n + 1 non-decreasing indices
+ * (d_seg_first[n] = nseg). Segments take the indexed path (bounds reported as for bkd_crc_batch);
+ * one GF(2) combine per segment joins them. Device pointers; asynchronous on `stream`. */
+int bkd_crc_batch_segments(int algo, const void* d_base, uint64_t base_size, const uint64_t* d_seg_offsets,
+                           const uint32_t* d_seg_lengths, uint64_t nseg, const uint64_t* d_seg_first, uint64_t n,
+                           const uint32_t* d_seeds, uint32_t seed_all, uint32_t* d_out, void* stream);
+
 /* Waits for `stream` and reports any bounds violation recorded by earlier indexed batches. */
 int bkd_stream_sync(void* stream);
 

@@ -504,3 +504,48 @@ def test_concurrent_callers(gpu):
     for t in threads:
         t.join()
     assert not errors, errors
+
+
+@pytest.mark.parametrize("size", [16383, 16384])
+@pytest.mark.parametrize("v2", [False, True])
+def test_composite_payload_digest_equals_contiguous(gpu, size, v2):
+    """CompositeByteBufUnwrapBugReproduceTest (:142-201): every composite wrapping of the payload
+    packages to the same bytes as the contiguous payload, and to the oracle's digest."""
+    from test_bytebuf import scenarios
+    payload = bytes(i & 0xFF for i in range(size))
+    for dtype, algo in ((dg.DigestType.CRC32C, ck.CRC32C), (dg.DigestType.CRC32, ck.CRC32)):
+        dm = dg.DigestManager.instantiate(1, b"", dtype, v2)
+        want = dm.computeDigestAndPackageForSending(1, 0, size, payload, b"\0" * 20, 0)
+        d, hdr = oracle.digest_entry(algo, 1, 1, 0, size, payload)
+        assert want.endswith(hdr + oracle.digest_bytes(algo, d) + payload)
+        for name, buf in scenarios(payload).items():
+            assert dm.computeDigestAndPackageForSending(1, 0, size, buf, b"\0" * 20, 0) == want, (name, algo)
+
+
+def test_crc_batch_segments(gpu):
+    """Composite entries on the device: each entry's digest equals the oracle's over the concatenation
+    of its segments (empty segments, single segments, many small and a few large pieces, seeds)."""
+    import torch
+    rng = np.random.default_rng(21)
+    size = 3 << 20
+    data = oracle.fill_splitmix64(size, 31)
+    base = _dev_bytes(torch, data, gpu)
+    n = 1500
+    counts = rng.integers(0, 9, n)
+    counts[:4] = [0, 1, 2, 40]
+    seg_first = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(counts, out=seg_first[1:])
+    nseg = int(seg_first[-1])
+    lens = rng.integers(0, 3000, nseg)
+    lens[rng.random(nseg) < 0.15] = 0
+    lens[rng.random(nseg) < 0.02] = 200_000
+    offs = np.array([int(rng.integers(0, size - l + 1)) for l in lens], dtype=np.int64)
+    seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    for algo in (ck.CRC32C, ck.CRC32):
+        got = ck.crc_batch_segments(algo, base, torch.from_numpy(offs).to(gpu),
+                                    torch.from_numpy(lens.astype(np.int32)).to(gpu), torch.from_numpy(seg_first).to(gpu),
+                                    seeds=torch.from_numpy(seeds.view(np.int32)).to(gpu), sync_check=True)
+        got = got.cpu().numpy().view(np.uint32)
+        for i in range(n):
+            cat = b"".join(data[offs[k]:offs[k] + lens[k]].tobytes() for k in range(seg_first[i], seg_first[i + 1]))
+            assert got[i] == oracle.resume(algo, int(seeds[i]), cat), (algo, i)
