@@ -703,9 +703,8 @@ int bkd_digest_package_batch(int algo, int64_t ledger_id, const int64_t* d_entry
     hipStream_t st = (hipStream_t)stream;
     const int lanes = auto_lanes(payload_size / n, n, ds->cus);
     const uint32_t* tab = ds->tables[algo][lane_index(lanes)];
-    const uint32_t* btab = tab + bkd::gf2::byte_table_offset(lanes);
     const unsigned blocks = (unsigned)((n + 255) / 256);
-    hipLaunchKernelGGL(bkd::package_header_kernel, dim3(blocks), dim3(256), 0, st, btab, ledger_id, d_entry_ids,
+    hipLaunchKernelGGL(bkd::package_header_kernel, dim3(blocks), dim3(256), 0, st, tab + 1024, ledger_id, d_entry_ids,
                        d_lacs, d_length_fields, n, (uint8_t*)d_frames, frame_stride, d_digests);
     BKD_HIP(hipGetLastError());
     bkd::IndexedSrc src{n, d_offsets, d_lengths, d_digests, 0u, payload_size, d_digests};
@@ -736,10 +735,11 @@ int verify_framed(int algo, int64_t ledger_id, int64_t first_entry_id, int id_ch
         BKD_HIP(hipMemsetAsync(d_first_bad, 0, sizeof(uint64_t), st));
         return BKD_OK;
     }
-    const uint32_t* btab = ds->tables[algo][lane_index(4)] + bkd::gf2::byte_table_offset(4);
+    const uint32_t* x32tab = ds->tables[algo][lane_index(4)] + 1024;  // x^32 operator, 4 x 256
     const unsigned blocks = (unsigned)((n + 255) / 256);
     Carver cv;
-    const size_t o_seeds = cv.take(n * 4), o_plen = cv.take(n * 4), o_poff = cv.take(n * 8);
+    const size_t o_seeds = cv.take(n * 4), o_plen = cv.take(n * 4), o_poff = cv.take(n * 8), o_exp = cv.take(n * 4),
+                 o_pre = cv.take(n * 4);
     StreamScratch& sc = scratch_for(*ds, st);
     std::lock_guard<std::recursive_mutex> lk(sc.mu);  // held across the nested plan (slot 0)
     uint8_t* sb = nullptr;
@@ -747,21 +747,22 @@ int verify_framed(int algo, int64_t ledger_id, int64_t first_entry_id, int id_ch
     uint32_t* seeds = Carver::at<uint32_t>(sb, o_seeds);
     uint32_t* plen = Carver::at<uint32_t>(sb, o_plen);
     uint64_t* poff = Carver::at<uint64_t>(sb, o_poff);
+    uint32_t* expect = Carver::at<uint32_t>(sb, o_exp);
+    uint32_t* pre = Carver::at<uint32_t>(sb, o_pre);
     if (e != hipSuccess) {
         rc = fail(BKD_ERR_NOMEM, std::string("verify scratch: ") + hipGetErrorString(e));
     } else {
-        hipLaunchKernelGGL(bkd::verify_header_kernel, dim3(blocks), dim3(256), 0, st, btab,
-                           (const uint8_t*)d_framed, framed_size, d_offsets, d_lengths, n, mac, seeds, poff, plen,
-                           d_first_bad);
+        hipLaunchKernelGGL(bkd::verify_header_kernel, dim3(blocks), dim3(256), 0, st, x32tab,
+                           (const uint8_t*)d_framed, framed_size, d_offsets, d_lengths, n, mac, ledger_id,
+                           first_entry_id, id_checks, seeds, poff, plen, expect, pre, d_first_bad);
         e = hipGetLastError();
         if (e != hipSuccess) rc = fail(BKD_ERR_HIP, hipGetErrorString(e));
         if (!rc)  // payload CRCs land in d_status, then verify_finish turns them into status codes
             rc = indexed_batch(*ds, algo, (const uint8_t*)d_framed, framed_size, poff, plen, n, seeds, 0,
                                reinterpret_cast<uint32_t*>(d_status), st);
         if (!rc) {
-            hipLaunchKernelGGL(bkd::verify_finish_kernel, dim3(blocks), dim3(256), 0, st, (const uint8_t*)d_framed,
-                               framed_size, d_offsets, d_lengths, n, mac, ledger_id, first_entry_id, id_checks,
-                               d_status, (unsigned long long*)d_first_bad);
+            hipLaunchKernelGGL(bkd::verify_finish_kernel, dim3(blocks), dim3(256), 0, st, expect, pre, n, d_status,
+                               (unsigned long long*)d_first_bad);
             e = hipGetLastError();
             if (e != hipSuccess) rc = fail(BKD_ERR_HIP, hipGetErrorString(e));
         }

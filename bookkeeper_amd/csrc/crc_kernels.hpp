@@ -692,123 +692,167 @@ __global__ void fill_splitmix64_kernel(uint8_t* __restrict__ dst, uint64_t nbyte
 
 // ---- DigestManager framing helpers (one thread per entry; 32-byte headers) ----
 
-__device__ __forceinline__ uint32_t crc_bytes_serial(const uint32_t* btab, uint32_t reg, const uint8_t* p,
-                                                     uint32_t len) {
-    for (uint32_t k = 0; k < len; ++k) reg = btab[(reg ^ p[k]) & 0xffu] ^ (reg >> 8);
-    return reg;
-}
-
-__device__ __forceinline__ void put_be64(uint8_t* p, uint64_t v) {
-#pragma unroll
-    for (int k = 7; k >= 0; --k) {
-        p[k] = (uint8_t)v;
-        v >>= 8;
-    }
-}
-
 // Package step 1: header [ledgerId, entryId, LAC, length] BE into the frame
-// (DigestManager.java:146-149 / :172-175) and its CRC (= the payload's seed) into seeds[i].
-__global__ void package_header_kernel(const uint32_t* __restrict__ byte_table, int64_t ledger_id,
-                                      const int64_t* __restrict__ entry_ids, const int64_t* __restrict__ lacs,
-                                      const int64_t* __restrict__ length_fields, uint64_t n,
-                                      uint8_t* __restrict__ frames, uint64_t frame_stride,
-                                      uint32_t* __restrict__ seeds) {
-    __shared__ uint32_t bt[256];
-    for (int k = threadIdx.x; k < 256; k += blockDim.x) bt[k] = byte_table[k];
+// (DigestManager.java:146-149 / :172-175) and its CRC (= the payload's seed) into seeds[i]. The
+// header is built as 8 little-endian dwords (byte-swapped BE fields), folded with the x^32 operator
+// (4 lookups per dword) and stored as dwords when the frame is 4-byte aligned.
+__global__ void __launch_bounds__(256) package_header_kernel(const uint32_t* __restrict__ x32tab, int64_t ledger_id,
+                                                             const int64_t* __restrict__ entry_ids,
+                                                             const int64_t* __restrict__ lacs,
+                                                             const int64_t* __restrict__ length_fields, uint64_t n,
+                                                             uint8_t* __restrict__ frames, uint64_t frame_stride,
+                                                             uint32_t* __restrict__ seeds) {
+    __shared__ uint32_t W[1024];
+    for (int k = threadIdx.x; k < 1024; k += blockDim.x) W[k] = x32tab[k];
     __syncthreads();
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    uint8_t h[32];
-    put_be64(h + 0, (uint64_t)ledger_id);
-    put_be64(h + 8, (uint64_t)entry_ids[i]);
-    put_be64(h + 16, (uint64_t)lacs[i]);
-    put_be64(h + 24, (uint64_t)length_fields[i]);
+    const uint64_t fld[4] = {(uint64_t)ledger_id, (uint64_t)entry_ids[i], (uint64_t)lacs[i],
+                             (uint64_t)length_fields[i]};
+    uint32_t w[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        w[2 * k] = __builtin_bswap32((uint32_t)(fld[k] >> 32));
+        w[2 * k + 1] = __builtin_bswap32((uint32_t)fld[k]);
+    }
+    uint32_t reg = 0xFFFFFFFFu;  // update(0, header)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t r = reg ^ w[k];
+        reg = W[r & 0xffu] ^ W[256 + ((r >> 8) & 0xffu)] ^ W[512 + ((r >> 16) & 0xffu)] ^ W[768 + (r >> 24)];
+    }
     uint8_t* f = frames + i * frame_stride;
-    for (int k = 0; k < 32; ++k) f[k] = h[k];
-    seeds[i] = ~crc_bytes_serial(bt, 0xFFFFFFFFu, h, 32);
+    if ((((uintptr_t)f) & 3u) == 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) reinterpret_cast<uint32_t*>(f)[k] = w[k];
+    } else {
+        for (int k = 0; k < 32; ++k) f[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+    }
+    seeds[i] = ~reg;
 }
 
 // Package step 3: the digest bytes after the header (CRC32CDigestManager.java:44-46: writeInt;
 // CRC32DigestManager.java:60-63: writeLong of the zero-extended value).
-__global__ void package_digest_kernel(const uint32_t* __restrict__ digests, uint64_t n, uint8_t* __restrict__ frames,
-                                      uint64_t frame_stride, uint32_t mac) {
+__global__ void __launch_bounds__(256) package_digest_kernel(const uint32_t* __restrict__ digests, uint64_t n,
+                                                             uint8_t* __restrict__ frames, uint64_t frame_stride,
+                                                             uint32_t mac) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint8_t* f = frames + i * frame_stride + 32;
-    const uint32_t d = digests[i];
-    if (mac == 8) {
-        f[0] = f[1] = f[2] = f[3] = 0;
-        f += 4;
+    const uint32_t be = __builtin_bswap32(digests[i]);
+    if ((((uintptr_t)f) & 3u) == 0) {
+        uint32_t* d = reinterpret_cast<uint32_t*>(f);
+        if (mac == 8) *d++ = 0u;
+        *d = be;
+    } else {
+        if (mac == 8) {
+            f[0] = f[1] = f[2] = f[3] = 0;
+            f += 4;
+        }
+        for (int k = 0; k < 4; ++k) f[k] = (uint8_t)(be >> (8 * k));
     }
-    f[0] = (uint8_t)(d >> 24);
-    f[1] = (uint8_t)(d >> 16);
-    f[2] = (uint8_t)(d >> 8);
-    f[3] = (uint8_t)d;
 }
 
-// Verify step 1: CRC of the 32-byte header of each framed entry (DigestManager.java:236), and the
-// payload range [o + 32 + mac, o + l) that step 2 folds from that seed (empty for a short entry).
-__global__ void verify_header_kernel(const uint32_t* __restrict__ byte_table, const uint8_t* __restrict__ framed,
-                                     uint64_t size, const uint64_t* __restrict__ offsets,
-                                     const uint32_t* __restrict__ lengths, uint64_t n, uint32_t mac,
-                                     uint32_t* __restrict__ seeds, uint64_t* __restrict__ pay_offsets,
-                                     uint32_t* __restrict__ pay_lengths, uint64_t* __restrict__ first_bad) {
-    __shared__ uint32_t bt[256];
-    for (int k = threadIdx.x; k < 256; k += blockDim.x) bt[k] = byte_table[k];
+// Verify step 1 (one thread per framed entry [32 B header][mac][payload], DigestManager.java:226-283):
+// reads the header and the stored digest once — 16-byte loads when the frame is 16-byte aligned,
+// dword loads when 4-byte aligned, bytes otherwise — and writes everything step 3 needs, so that
+// step 3 touches no frame bytes:
+//   seeds[i]   CRC of the 32-byte header = the payload's seed (:236)
+//   pay_*[i]   the payload range [o + 32 + mac, o + l) step 2 folds (empty for a short entry)
+//   expect[i]  the stored digest (low 32 bits; CRC32DigestManager writes a zero-extended long)
+//   pre[i]     1 too short / out of range (:229-235); else bit 1 = high digest word non-zero,
+//              bits 2.. = the id check's code (3 ledger mismatch :267-273, 4 entry mismatch :275-281)
+// The header CRC folds 8 little-endian dwords with the x^32 operator (4 lookups per dword).
+__device__ __forceinline__ uint32_t be32_at(const uint32_t* w, int byte) {  // big-endian u32 at a 4-aligned byte
+    return __builtin_bswap32(w[byte >> 2]);
+}
+
+__global__ void __launch_bounds__(256) verify_header_kernel(const uint32_t* __restrict__ x32tab,
+                                                            const uint8_t* __restrict__ framed, uint64_t size,
+                                                            const uint64_t* __restrict__ offsets,
+                                                            const uint32_t* __restrict__ lengths, uint64_t n,
+                                                            uint32_t mac, int64_t ledger_id, int64_t first_entry_id,
+                                                            int id_checks, uint32_t* __restrict__ seeds,
+                                                            uint64_t* __restrict__ pay_offsets,
+                                                            uint32_t* __restrict__ pay_lengths,
+                                                            uint32_t* __restrict__ expect, uint32_t* __restrict__ pre,
+                                                            uint64_t* __restrict__ first_bad) {
+    __shared__ uint32_t W[1024];
+    for (int k = threadIdx.x; k < 1024; k += blockDim.x) W[k] = x32tab[k];
     __syncthreads();
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0) *first_bad = n;
     if (i >= n) return;
     const uint64_t o = offsets[i];
     const uint32_t l = lengths[i];
-    uint32_t s = 0;
-    uint64_t po = 0;
-    uint32_t pl = 0;
-    if (o <= size && (uint64_t)l <= size - o && l >= 32u + mac) {
-        s = ~crc_bytes_serial(bt, 0xFFFFFFFFu, framed + o, 32);
-        po = o + 32u + mac;
-        pl = l - 32u - mac;
+    if (o > size || (uint64_t)l > size - o || l < 32u + mac) {
+        seeds[i] = 0u;
+        pay_offsets[i] = 0u;
+        pay_lengths[i] = 0u;
+        expect[i] = 0u;
+        pre[i] = 1u;
+        return;
     }
-    seeds[i] = s;
-    pay_offsets[i] = po;
-    pay_lengths[i] = pl;
+    const uint8_t* f = framed + o;
+    uint32_t w[10];  // bytes [0, 40) of the frame as little-endian dwords (the first 32 + mac are used)
+    const int nw = (int)(32u + mac) / 4;
+    if ((((uintptr_t)f) & 15u) == 0 && l >= 48u) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const u32x4 v = *reinterpret_cast<const u32x4*>(f + 16 * k);
+            if (4 * k < 10) w[4 * k] = v.x;
+            if (4 * k + 1 < 10) w[4 * k + 1] = v.y;
+            if (4 * k + 2 < 10) w[4 * k + 2] = v.z;
+            if (4 * k + 3 < 10) w[4 * k + 3] = v.w;
+        }
+    } else if ((((uintptr_t)f) & 3u) == 0) {
+        for (int k = 0; k < 10; ++k) w[k] = k < nw ? reinterpret_cast<const uint32_t*>(f)[k] : 0u;
+    } else {
+        for (int k = 0; k < 10; ++k) {
+            uint32_t v = 0u;
+            if (k < nw)
+                for (int b = 3; b >= 0; --b) v = (v << 8) | f[4 * k + b];
+            w[k] = v;
+        }
+    }
+    uint32_t reg = 0xFFFFFFFFu;  // update(0, header): resume from 0 = register ~0
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t r = reg ^ w[k];
+        reg = W[r & 0xffu] ^ W[256 + ((r >> 8) & 0xffu)] ^ W[512 + ((r >> 16) & 0xffu)] ^ W[768 + (r >> 24)];
+    }
+    seeds[i] = ~reg;
+    pay_offsets[i] = o + 32u + mac;
+    pay_lengths[i] = l - 32u - mac;
+    const uint64_t lid = ((uint64_t)be32_at(w, 0) << 32) | be32_at(w, 4);
+    const uint64_t eid = ((uint64_t)be32_at(w, 8) << 32) | be32_at(w, 12);
+    uint32_t p = 0u;
+    if (mac == 8) {
+        if (w[8] != 0u) p |= 2u;
+        expect[i] = be32_at(w, 36);
+    } else {
+        expect[i] = be32_at(w, 32);
+    }
+    // id_checks: 0 ledger + entry ids, 1 ledger id only, 2 digest only (entry-log scrub)
+    if (id_checks < 2 && (int64_t)lid != ledger_id) p |= 3u << 2;
+    else if (id_checks == 0 && (int64_t)eid != first_entry_id + (int64_t)i) p |= 4u << 2;
+    pre[i] = p;
 }
 
-// Verify step 3: compare digest bytes and ids, per-entry status, first failing index
-// (DigestManager.java:241-281; BatchedReadOp.java:164-190 verified-prefix rule).
-__global__ void verify_finish_kernel(const uint8_t* __restrict__ framed, uint64_t size,
-                                     const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ lengths,
-                                     uint64_t n, uint32_t mac, int64_t ledger_id, int64_t first_entry_id,
-                                     int skip_entry_check, int32_t* __restrict__ status,
-                                     unsigned long long* __restrict__ first_bad) {
+// Verify step 3: per-entry status in DigestManager.verifyDigest's order (too short, digest, ledger id,
+// entry id) and the first failing index (BatchedReadOp.java:164-190 verified-prefix rule).
+__global__ void __launch_bounds__(256) verify_finish_kernel(const uint32_t* __restrict__ expect,
+                                                            const uint32_t* __restrict__ pre, uint64_t n,
+                                                            int32_t* __restrict__ status,
+                                                            unsigned long long* __restrict__ first_bad) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t computed = (uint32_t)status[i];
-    const uint64_t o = offsets[i];
-    const uint32_t l = lengths[i];
-    int32_t st = 0;
-    if (o > size || (uint64_t)l > size - o || l < 32u + mac) {
-        st = 1;
-    } else {
-        const uint8_t* f = framed + o;
-        uint32_t stored;
-        bool hi_zero = true;
-        if (mac == 8) {
-            hi_zero = (f[32] | f[33] | f[34] | f[35]) == 0;
-            stored = ((uint32_t)f[36] << 24) | ((uint32_t)f[37] << 16) | ((uint32_t)f[38] << 8) | f[39];
-        } else {
-            stored = ((uint32_t)f[32] << 24) | ((uint32_t)f[33] << 16) | ((uint32_t)f[34] << 8) | f[35];
-        }
-        uint64_t lid = 0, eid = 0;
-        for (int k = 0; k < 8; ++k) {
-            lid = (lid << 8) | f[k];
-            eid = (eid << 8) | f[8 + k];
-        }
-        // skip_entry_check: 0 ledger + entry ids, 1 ledger id only, 2 digest only (entry-log scrub)
-        if (!hi_zero || stored != computed) st = 2;
-        else if (skip_entry_check < 2 && (int64_t)lid != ledger_id) st = 3;
-        else if (skip_entry_check == 0 && (int64_t)eid != first_entry_id + (int64_t)i) st = 4;
-    }
+    const uint32_t p = pre[i];
+    int32_t st;
+    if (p == 1u) st = 1;
+    else if ((p & 2u) || computed != expect[i]) st = 2;
+    else st = (int32_t)(p >> 2);
     status[i] = st;
     if (st != 0) atomicMin(first_bad, (unsigned long long)i);
 }
