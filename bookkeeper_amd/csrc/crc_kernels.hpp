@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace bkd {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -388,6 +390,101 @@ __device__ __forceinline__ void groups_loop(const uint32_t* lds, uint32_t lanere
     }
 }
 
+// Uniform batches of short entries (16 B <= len <= 16*G*(PF+1), every load of an entry fits one
+// register set): a group's next entry is loaded while the current one folds (X/Y register sets),
+// so a wave no longer waits one HBM round trip per entry — the one-entry-per-group loop is
+// latency-bound there (its rate falls in proportion to G at 64 B: profiles/r01_size_sweep.log).
+struct SmallGeo {
+    int64_t s, a, la0;  // entry start, this lane's step-0 block, its load address (>= s, in bounds)
+    uint32_t J;
+    uint32_t r0;
+};
+
+template <int G>
+__device__ __forceinline__ SmallGeo small_geo(const UniformSrc& src, uint64_t i, int g) {
+    SmallGeo c;
+    c.s = (int64_t)(i * src.stride);
+    c.J = (src.len + (uint32_t)Geo<G>::kStep - 1u) / (uint32_t)Geo<G>::kStep;
+    c.a = c.s + (int64_t)src.len - (int64_t)c.J * Geo<G>::kStep + 16 * g;
+    c.la0 = c.a >= c.s ? c.a : c.s;  // the straddling lane loads at s and shifts; lanes before s reload s
+    c.r0 = ~(src.seeds ? src.seeds[i] : src.seed_all);
+    return c;
+}
+
+template <int G, int PF, bool NT>
+__device__ __forceinline__ void small_load(const uint8_t* __restrict__ base, const SmallGeo& c, u32x4& W0,
+                                           u32x4 (&A)[PF]) {
+    W0 = ld16<NT>(base + c.la0);
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {
+        const int64_t addr = (uint32_t)(k + 1) < c.J ? c.a + (int64_t)(k + 1) * Geo<G>::kStep : c.la0;
+        A[k] = ld16<NT>(base + addr);
+    }
+}
+
+// Raw register of a short entry from its loaded blocks (fold_range's arithmetic, J <= PF + 1).
+template <int G, int PF>
+__device__ __forceinline__ uint32_t small_fold(const uint32_t* lds, uint32_t lanereg, const SmallGeo& c, u32x4 W0,
+                                               const u32x4 (&A)[PF]) {
+    using Gm = Geo<G>;
+    const int64_t s = c.s, a = c.a;
+    u32x4 w;
+    if (a >= s) w = W0;
+    else if (a + 16 > s) w = shl_bytes(W0, (uint32_t)(s - a));
+    else w = u32x4{0u, 0u, 0u, 0u};
+    const uint32_t r0 = c.r0;
+    if (a < s + 4 && a + 16 > s) {
+        const int64_t d = s - a;
+        w.x ^= place_seed(r0, d);
+        w.y ^= place_seed(r0, d - 4);
+        w.z ^= place_seed(r0, d - 8);
+        w.w ^= place_seed(r0, d - 12);
+    }
+    uint32_t fx = 0u;
+    if (a + Gm::kStep < s + 4) fx = place_seed(r0, s - (a + Gm::kStep));
+    uint32_t c0 = w.x, c1 = w.y, c2 = w.z, c3 = w.w;
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {
+        if ((uint32_t)(k + 1) < c.J) {
+            c0 = mul_main(lds, c0, lanereg) ^ A[k].x ^ (k == 0 ? fx : 0u);
+            c1 = mul_main(lds, c1, lanereg) ^ A[k].y;
+            c2 = mul_main(lds, c2, lanereg) ^ A[k].z;
+            c3 = mul_main(lds, c3, lanereg) ^ A[k].w;
+        }
+    }
+    return finish_lanes<G>(lds, c0, c1, c2, c3);
+}
+
+template <int G, int PF, bool NT>
+__device__ __forceinline__ void uniform_small_loop(const uint32_t* lds, uint32_t lanereg, int g,
+                                                   const uint8_t* __restrict__ base, const UniformSrc& src, uint64_t n,
+                                                   uint64_t gid, uint64_t ngroups) {
+    u32x4 W0x, Ax[PF], W0y, Ay[PF];
+    SmallGeo cx = small_geo<G>(src, gid, g), cy;
+    small_load<G, PF, NT>(base, cx, W0x, Ax);
+    for (uint64_t i = gid;;) {
+        // entry i in set X; entry i + ngroups (if any) loads into Y meanwhile
+        uint64_t j = i + ngroups;
+        if (j < n) {
+            cy = small_geo<G>(src, j, g);
+            small_load<G, PF, NT>(base, cy, W0y, Ay);
+        }
+        uint32_t v = small_fold<G, PF>(lds, lanereg, cx, W0x, Ax);
+        if (g == 0) src.out[i] = ~v;
+        if (j >= n) break;
+        i = j;
+        j = i + ngroups;
+        if (j < n) {
+            cx = small_geo<G>(src, j, g);
+            small_load<G, PF, NT>(base, cx, W0x, Ax);
+        }
+        v = small_fold<G, PF>(lds, lanereg, cy, W0y, Ay);
+        if (g == 0) src.out[i] = ~v;
+        if (j >= n) break;
+        i = j;
+    }
+}
+
 // One CRC per work item of `src` (uniform / indexed / framed-payload entries), persistent grid.
 template <int G, int PF, bool NT, class Src>
 __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __restrict__ base, Src src,
@@ -404,6 +501,12 @@ __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __res
     const uint32_t lanereg = ((uint32_t)(lane & 31) << 2) | (1u << 16);
     const uint64_t ngroups = (uint64_t)gridDim.x * (kBlock / G);
     const uint64_t gid = (uint64_t)blockIdx.x * (kBlock / G) + (uint64_t)(threadIdx.x / G);
+    if constexpr (std::is_same<Src, UniformSrc>::value) {
+        if (src.len >= 16u && src.len <= (uint32_t)Gm::kStep * (uint32_t)(PF + 1)) {
+            if (gid < n) uniform_small_loop<G, PF, NT>(lds, lanereg, g, base, src, n, gid, ngroups);
+            return;
+        }
+    }
     groups_loop<G, PF, NT>(lds, lanereg, g, base, src, n, gid, ngroups, err);
 }
 

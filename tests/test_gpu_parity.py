@@ -124,6 +124,27 @@ def test_uniform_batches(gpu, algo, lanes):
         assert (got.cpu().numpy().view(np.uint32) == want).all(), (entry_len, stride, n)
 
 
+@pytest.mark.parametrize("lanes", LANES)
+def test_uniform_short_entries_seeded(gpu, lanes):
+    """Short uniform entries take the pipelined short-entry loop (every load of an entry in one
+    register set, the next entry loaded during the fold); per-entry seeds, unaligned strides, and
+    batches smaller and larger than the grid."""
+    import torch
+    ck.set_group_lanes(lanes)
+    rng = np.random.default_rng(lanes)
+    for entry_len, stride, n in [(16, 16, 5), (20, 23, 70001), (64, 64, 300000), (127, 131, 4097),
+                                 (16 * lanes * 3, 16 * lanes * 3 + 5, 20000), (16 * lanes * 3 + 1, 16 * lanes * 3 + 1, 999)]:
+        nbytes = (n - 1) * stride + entry_len
+        data = oracle.fill_splitmix64(nbytes, entry_len + lanes)
+        base = _dev_bytes(torch, data, gpu)
+        seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        got = ck.crc_batch_uniform(ck.CRC32C, base, entry_len, n, stride=stride,
+                                   seeds=torch.from_numpy(seeds.view(np.int32)).to(gpu))
+        offs = np.arange(n, dtype=np.uint64) * stride
+        want = oracle.batch(ck.CRC32C, data, offs, np.full(n, entry_len, dtype=np.uint32), seeds=seeds)
+        assert (got.cpu().numpy().view(np.uint32) == want).all(), (entry_len, stride, n)
+
+
 @pytest.mark.parametrize("algo", [ck.CRC32C, ck.CRC32])
 @pytest.mark.parametrize("lanes,mode", [(l, 1) for l in LANES] + [(0, 2), (0, 0)])
 def test_indexed_ragged_unaligned(gpu, algo, lanes, mode):

@@ -41,7 +41,7 @@ def main(paths):
     base = torch.empty(max(total, n * 4096), dtype=torch.uint8, device=dev)
     first = next(iter(libs.values()))
     first.bkd_fill_splitmix64(ctypes.c_void_p(base.data_ptr()), base.numel(), 42, 0, None)
-    out = torch.empty(n, dtype=torch.int32, device=dev)
+    out = torch.empty(max(n, (4 << 30) // 64), dtype=torch.int32, device=dev)
     ptr = lambda t: ctypes.c_void_p(t.data_ptr())
 
     def idx(o, l):
@@ -57,14 +57,25 @@ def main(paths):
         "indexed4k": (0, *idx(np.arange(n) * 4096, np.full(n, 4096)), n * 4096),
     }
 
+    small = {f"u{S}_l{G}": (S, G) for S, G in ((64, 4), (64, 8), (128, 4), (128, 8), (256, 4), (256, 8), (512, 8),
+                                               (1024, 8))}
+
     def call(L, name):
         if name == "uniform4k":
+            L.bkd_set_group_lanes(0)
             return L.bkd_crc_batch_uniform(0, ptr(base), 4096, 4096, n, None, 0, ptr(out), ctypes.c_void_p(st.cuda_stream))
+        if name in small:
+            S, G = small[name]
+            L.bkd_set_group_lanes(G)
+            r = L.bkd_crc_batch_uniform(0, ptr(base), S, S, (4 << 30) // S, None, 0, ptr(out),
+                                        ctypes.c_void_p(st.cuda_stream))
+            L.bkd_set_group_lanes(0)
+            return r
         algo, o, l, _ = work[name]
         return L.bkd_crc_batch(algo, ptr(base), base.numel(), ptr(o), ptr(l), o.numel(), None, 0, ptr(out),
                                ctypes.c_void_p(st.cuda_stream))
 
-    names = list(work) + ["uniform4k"]
+    names = [w for w in os.environ.get("AB_WORK", " ".join(list(work) + ["uniform4k"] + list(small))).split()]
     res = {}
     for name in names:
         ref = None
@@ -72,7 +83,7 @@ def main(paths):
             L.bkd_set_plan_mode(0)
             assert call(L, name) == 0, name
             torch.cuda.synchronize()
-            cnt = work[name][1].numel() if name in work else n
+            cnt = work[name][1].numel() if name in work else ((4 << 30) // small[name][0] if name in small else n)
             if ref is None:
                 ref = out[:cnt].clone()
             assert torch.equal(out[:cnt], ref), f"{name}: digests differ between libraries"
@@ -85,7 +96,7 @@ def main(paths):
                 e1.record(st)
                 torch.cuda.synchronize()
                 res.setdefault((name, lname), []).append(e0.elapsed_time(e1) / REPS)
-        nbytes = work[name][3] if name in work else n * 4096
+        nbytes = work[name][3] if name in work else (4 << 30 if name in small else n * 4096)
         for lname in libs:
             v = sorted(res[(name, lname)])
             print(f"{name:12s} {lname:22s} median {v[len(v) // 2]:.4f} ms  min {v[0]:.4f} ms  "
