@@ -99,3 +99,28 @@ def test_plan_chunk_combine_model(algo):
             got = plan_model(tabs, lambda nb: oracle.xpow8n(algo, nb), lambda a, b: oracle.gf_mul(algo, a, b), d,
                              seed, lanes=4, jc=jc, mis=mis)
             assert got == oracle.resume(algo, seed, d), (n, mis)
+
+
+@pytest.mark.parametrize("algo", [0, 1])
+def test_segments_join_model(algo):
+    """bkd_crc_batch_segments' join (plan_kernels.hpp segments_combine_kernel) on CPU: each segment's
+    zero-initialised register is ~resume(~0, segment) (the indexed path with seed ~0); the entry is
+    reg = ~seed, then per non-empty segment reg = reg * x^(8 len) ^ raw, the power taken as the
+    product of x^(8 * 2^b) over the set bits of len — equal to resume(seed, concatenation)."""
+    rng = np.random.default_rng(40 + algo)
+    pw = [oracle.xpow8n(algo, 1 << b) for b in range(32)]
+    for _ in range(40):
+        segs = [rng.integers(0, 256, int(rng.choice([0, 1, 3, 16, 100, 4097])), dtype=np.uint8).tobytes()
+                for _ in range(int(rng.integers(0, 6)))]
+        seed = int(rng.integers(0, 2**32))
+        reg = (~seed) & 0xFFFFFFFF
+        for sg in segs:
+            if not sg:
+                continue
+            raw = (~oracle.resume(algo, 0xFFFFFFFF, sg)) & 0xFFFFFFFF
+            n = len(sg)
+            for b in range(32):
+                if (n >> b) & 1:
+                    reg = oracle.gf_mul(algo, pw[b], reg)
+            reg ^= raw
+        assert (~reg) & 0xFFFFFFFF == oracle.resume(algo, seed, b"".join(segs))
