@@ -37,8 +37,8 @@ constexpr uint32_t kMainBytes = 131072u;  // 4 tables x 256 entries x 32 banks x
 
 template <int G>
 struct Geo {
-    static_assert(G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "group width");
-    static constexpr int kLevels = G == 4 ? 2 : G == 8 ? 3 : G == 16 ? 4 : G == 32 ? 5 : 6;
+    static_assert(G == 1 || G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "group width");
+    static constexpr int kLevels = G == 1 ? 0 : G == 4 ? 2 : G == 8 ? 3 : G == 16 ? 4 : G == 32 ? 5 : 6;
     // Groups of <= 16 lanes sit inside one DPP row and have LDS room for the x^64/x^96 sets.
     static constexpr bool kFast = G <= 16;
     static constexpr int kCompactWords = (2 + kLevels) * 1024 + 256 + 2048;
@@ -213,7 +213,12 @@ template <int G>
 __device__ __forceinline__ uint32_t finish_lanes(const uint32_t* lds, uint32_t c0, uint32_t c1, uint32_t c2,
                                                  uint32_t c3) {
     using Gm = Geo<G>;
-    if constexpr (Gm::kFast) {
+    if constexpr (G == 1) {
+        // one lane per entry: x^128 is the main operator itself (replicated, conflict-free); no tree
+        const uint32_t lanereg = ((uint32_t)(threadIdx.x & 31) << 2) | (1u << 16);
+        return mul_main(lds, c0, lanereg) ^ mul_aux(lds, Gm::kX96Off, c1) ^ mul_aux(lds, Gm::kX64Off, c2) ^
+               mul_aux(lds, Gm::kX32Off, c3);
+    } else if constexpr (Gm::kFast) {
         const uint32_t v = mul_aux(lds, Gm::kX32Off + 4096u, c0) ^ mul_aux(lds, Gm::kX96Off, c1) ^
                            mul_aux(lds, Gm::kX64Off, c2) ^ mul_aux(lds, Gm::kX32Off, c3);
         return lane_tree_dpp<0, Gm::kLevels>(lds, Gm::kX32Off, v);

@@ -184,7 +184,7 @@ int64_t bkd_host_tables(int algo, int lanes, uint32_t* out, uint64_t out_words);
 uint32_t bkd_host_gf_mul(int algo, uint32_t a, uint32_t b);
 uint32_t bkd_host_xpow8n(int algo, uint64_t nbytes);
 
-/* Tuning: lanes per entry group (0 = automatic, else 4/8/16/32/64); prefetch is fixed at build. */
+/* Tuning: lanes per entry group (0 = automatic, else 1/4/8/16/32/64); prefetch is fixed at build. */
 int bkd_set_group_lanes(int lanes);
 /* Indexed-batch strategy: 0 = automatic (chunked plan unless the base buffer is <= 256 KiB),
  * 1 = one entry per lane group, 2 = always the chunked plan. */

@@ -17,7 +17,7 @@ from bookkeeper_amd._native import BkdError
 
 pytestmark = pytest.mark.gpu
 
-LANES = (4, 8, 16, 32, 64)
+LANES = (1, 4, 8, 16, 32, 64)
 
 
 @pytest.fixture(autouse=True)
@@ -143,6 +143,20 @@ def test_uniform_short_entries_seeded(gpu, lanes):
         offs = np.arange(n, dtype=np.uint64) * stride
         want = oracle.batch(ck.CRC32C, data, offs, np.full(n, entry_len, dtype=np.uint32), seeds=seeds)
         assert (got.cpu().numpy().view(np.uint32) == want).all(), (entry_len, stride, n)
+
+
+def test_uniform_tiny_entries_auto_one_lane(gpu):
+    """16..48-byte uniform entries in large batches pick one lane per entry automatically."""
+    import torch
+    for entry_len, stride in [(16, 16), (32, 32), (48, 50), (33, 40)]:
+        n = 300_000
+        nbytes = (n - 1) * stride + entry_len
+        data = oracle.fill_splitmix64(nbytes, entry_len)
+        base = _dev_bytes(torch, data, gpu)
+        for algo in (ck.CRC32C, ck.CRC32):
+            got = ck.crc_batch_uniform(algo, base, entry_len, n, stride=stride, seed_all=0x1234567)
+            want = oracle.uniform(algo, data, stride, entry_len, n, 0x1234567)
+            assert (got.cpu().numpy().view(np.uint32) == want).all(), (entry_len, stride, algo)
 
 
 @pytest.mark.parametrize("algo", [ck.CRC32C, ck.CRC32])

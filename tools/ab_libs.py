@@ -41,7 +41,6 @@ def main(paths):
     base = torch.empty(max(total, n * 4096), dtype=torch.uint8, device=dev)
     first = next(iter(libs.values()))
     first.bkd_fill_splitmix64(ctypes.c_void_p(base.data_ptr()), base.numel(), 42, 0, None)
-    out = torch.empty(max(n, (4 << 30) // 64), dtype=torch.int32, device=dev)
     ptr = lambda t: ctypes.c_void_p(t.data_ptr())
 
     def idx(o, l):
@@ -57,8 +56,13 @@ def main(paths):
         "indexed4k": (0, *idx(np.arange(n) * 4096, np.full(n, 4096)), n * 4096),
     }
 
-    small = {f"u{S}_l{G}": (S, G) for S, G in ((64, 4), (64, 8), (128, 4), (128, 8), (256, 4), (256, 8), (512, 8),
+    small = {f"u{S}_l{G}": (S, G) for S, G in ((32, 1), (32, 4), (64, 1), (64, 4), (64, 8), (128, 1), (128, 4),
+                                               (128, 8), (256, 1), (256, 4), (256, 8), (512, 1), (512, 4), (512, 8),
                                                (1024, 8))}
+
+    # one digest per entry of the largest batch (4 GiB of the smallest uniform size)
+    out = torch.empty(max(n, max((4 << 30) // S for S, _ in small.values())), dtype=torch.int32, device=dev)
+    assert base.numel() >= 4 << 30
 
     def call(L, name):
         if name == "uniform4k":
