@@ -364,11 +364,13 @@ __device__ __forceinline__ uint32_t gf_pow_bits(uint32_t x, uint32_t e, uint32_t
 }
 
 // Horner over the partial registers of each chunked entry, then x^(-8*pad); serial fold of
-// entries the plan did not chunk. Entries with more than kCombineSerial chunks (e.g. one 64 MiB
-// entry = 16 Ki chunks) are combined by the whole block instead of one serial thread: thread t
-// folds its contiguous run of partials with Horner (table X in LDS), is placed by X^(first chunk
-// of its run) (bitwise power), and the block XOR-reduces.
+// entries the plan did not chunk. Entries with more than kCombineSerial chunks are combined by a
+// wave (up to kCombineWave chunks) or by the whole block (e.g. one 64 MiB entry = 16 Ki chunks)
+// instead of one serial thread: thread t folds its contiguous run of partials with Horner (table
+// X in LDS), is placed by X^(first chunk of its run) (bitwise power), and the wave or block
+// XOR-reduces.
 constexpr uint32_t kCombineSerial = 64;
+constexpr uint32_t kCombineWave = 4096;
 
 __device__ __forceinline__ uint32_t mul_x(const uint32_t* X, uint32_t r) {
     return X[r & 0xffu] ^ X[256 + ((r >> 8) & 0xffu)] ^ X[512 + ((r >> 16) & 0xffu)] ^ X[768 + (r >> 24)];
@@ -435,10 +437,30 @@ __global__ void __launch_bounds__(1024) plan_combine_kernel(
     }
     __syncthreads();
     const uint32_t nb = nbig;
+    // 65 .. kCombineWave chunks: one wave per entry, the block's waves in parallel (4096 x 1 MiB
+    // entries leave 4 blocks of 1024 such entries each; one entry at a time per block took 8 ms)
+    const uint32_t lane = threadIdx.x & 63u, nwaves = blockDim.x >> 6;
+    for (uint32_t k = threadIdx.x >> 6; k < nb; k += nwaves) {
+        const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + big[k];
+        const EntryPlan p = plan_entry(offsets[e], lengths[e], size, pg);
+        if (p.m > kCombineWave) continue;  // wave-uniform
+        const uint32_t sl = pslot[e];
+        const uint32_t per = (p.m + 63u) >> 6;
+        const uint32_t lo = lane * per;
+        const uint32_t hi = lo + per < p.m ? lo + per : p.m;
+        uint32_t r = 0u;
+        for (int c = (int)hi - 1; c >= (int)lo; --c) r = mul_x(X, r) ^ partials[sl + (uint32_t)c];
+        if (lo < hi && lo) r = gf_mul_bits(gf_pow_bits(xval, lo, poly), r, poly);
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) r ^= (uint32_t)__shfl_xor((int)r, d);
+        if (lane == 0u) out[e] = ~(p.pad ? gf_mul_bits(xinv[p.pad], r, poly) : r);
+    }
+    // more chunks (entries of >= 16 MiB at 4 KiB chunks): the whole block per entry
     for (uint32_t k = 0; k < nb; ++k) {
         const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + big[k];
-        const uint32_t sl = pslot[e];
         const EntryPlan p = plan_entry(offsets[e], lengths[e], size, pg);
+        if (p.m <= kCombineWave) continue;  // block-uniform
+        const uint32_t sl = pslot[e];
         const uint32_t per = (p.m + blockDim.x - 1u) / blockDim.x;
         const uint32_t lo = threadIdx.x * per;
         const uint32_t hi = lo + per < p.m ? lo + per : p.m;

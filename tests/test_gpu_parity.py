@@ -343,6 +343,36 @@ def test_plan_overflow_falls_back_to_direct(gpu):
     assert (got.cpu().numpy().view(np.uint32) == oracle.batch(0, data, offs, lens, seed_all=0x1234)).all()
 
 
+def test_plan_mid_size_entries_wave_combine(gpu):
+    """Entries of 65..4096 chunks (256 KiB .. 16 MiB at 4 KiB chunks) are combined one wave per
+    entry, larger ones by the whole block: lengths around both thresholds, several such entries in
+    one combine block and across the 1024-entry block boundary, packed at odd offsets, seeded."""
+    import torch
+    ck.set_plan_mode(2)
+    rng = np.random.default_rng(65)
+    n = 1100
+    lens = rng.integers(0, 5000, n).astype(np.int64)
+    big = np.arange(3, n, 37)
+    lens[big] = rng.integers(64 * 4096 - 300, 1 << 20, big.size)
+    edges = [64 * 4096 - 128, 64 * 4096, 64 * 4096 + 1, 64 * 4096 + 200, 4096 * 4096 - 130, 4096 * 4096,
+             4096 * 4096 + 1, 4096 * 4096 + 4096 * 3]
+    for k, L in enumerate(edges):
+        lens[1010 + 2 * k] = L  # straddles the combine kernel's block boundary at entry 1024
+    offs = np.zeros(n, dtype=np.int64)
+    offs[1:] = np.cumsum(lens[:-1] + rng.integers(0, 200, n - 1))
+    size = int(offs[-1] + lens[-1] + 77)
+    base = torch.empty(size, dtype=torch.uint8, device=gpu)
+    ck.fill_splitmix64(base, 66)
+    host = base.cpu().numpy()
+    seeds = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    d_off, d_len = torch.from_numpy(offs).to(gpu), torch.from_numpy(lens.astype(np.int32)).to(gpu)
+    d_seed = torch.from_numpy(seeds.view(np.int32)).to(gpu)
+    for algo in (ck.CRC32C, ck.CRC32):
+        got = ck.crc_batch(algo, base, d_off, d_len, seeds=d_seed, sync_check=True).cpu().numpy().view(np.uint32)
+        want = oracle.batch(algo, host, offs, lens, seeds=seeds)
+        assert (got == want).all(), np.flatnonzero(got != want)[:10]
+
+
 def test_plan_huge_single_entry_and_small_neighbours(gpu):
     """A 96 MiB entry next to tiny ones: the plan spreads the big entry over the whole chip."""
     import torch
