@@ -299,8 +299,10 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     hipLaunchKernelGGL(bkd::plan_count_kernel, dim3(nb), dim3(bkd::kPlanBlock), 0, st, offsets, lengths, size, n, pg,
                        blk);
     hipLaunchKernelGGL(bkd::plan_scan_kernel, dim3(ncols), dim3(64), 0, st, blk, nb, blkoff, hdr);
-    hipLaunchKernelGGL(bkd::plan_emit_kernel, dim3(nb), dim3(bkd::kPlanBlock), 0, st, offsets, lengths, seeds,
-                       seed_all, size, n, pg, capacity, blkoff, pslot, hdr, descs);
+    // few entry blocks (large entries): replicate emit and combine blocks so ~2 blocks per CU work
+    const uint32_t reps = nb >= 2u * (uint32_t)ds.cus ? 1u : std::min<uint32_t>(64u, (2u * (uint32_t)ds.cus + nb - 1u) / nb);
+    hipLaunchKernelGGL(bkd::plan_emit_kernel, dim3(nb * reps), dim3(bkd::kPlanBlock), 0, st, offsets, lengths, seeds,
+                       seed_all, size, n, pg, capacity, blkoff, pslot, hdr, descs, reps);
     const uint32_t* tab = ds.tables[algo][lane_index(G)];
     const bkd::PlanDirectSrc ov{n, offsets, lengths, seeds, seed_all, size, out, pslot, hdr, capacity};
     switch (G) {
@@ -311,9 +313,9 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
         default: launch_plan_chunks<64>(base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st); break;
     }
     const uint32_t* btab = tab + bkd::gf2::byte_table_offset(G);
-    hipLaunchKernelGGL(bkd::plan_combine_kernel, dim3(nb), dim3(1024), 0, st, base, offsets, lengths, seeds, seed_all,
-                       size, n, pg, xtab, bkd::gf2::xpow(algo, 8ull * pg.ch), tab + 1024, btab, ds.xinv[algo],
-                       bkd::gf2::poly(algo), pslot, partials, out, ds.err);
+    hipLaunchKernelGGL(bkd::plan_combine_kernel, dim3(nb * reps), dim3(1024), 0, st, base, offsets, lengths, seeds,
+                       seed_all, size, n, pg, xtab, bkd::gf2::xpow(algo, 8ull * pg.ch), tab + 1024, btab, ds.xinv[algo],
+                       bkd::gf2::poly(algo), pslot, partials, out, ds.err, reps);
     e = hipGetLastError();
     if (e != hipSuccess) return fail(BKD_ERR_HIP, std::string("plan kernels: ") + hipGetErrorString(e));
     return BKD_OK;

@@ -238,12 +238,17 @@ __global__ void __launch_bounds__(kPlanBlock) plan_emit_kernel(const uint64_t* _
                                                                uint64_t size, uint64_t n, PlanGeo pg,
                                                                uint64_t capacity, const uint32_t* __restrict__ blkoff,
                                                                uint32_t* __restrict__ pslot, uint32_t* __restrict__ hdr,
-                                                               PlanDesc* __restrict__ descs) {
+                                                               PlanDesc* __restrict__ descs, uint32_t reps) {
+    // `reps` blocks per 1024-entry block (few entries, many chunks each: 256 x 16 MiB is one entry
+    // block): every replica plans the same entries, replica 0 writes heads, slots and the header,
+    // and the replicas split the block's full-chunk descriptors
+    const uint32_t eb = blockIdx.x / reps, rep = blockIdx.x - eb * reps, neb = gridDim.x / reps;
     __shared__ uint32_t wsum[kPlanBlock / 64 + 1];
     __shared__ uint32_t cursor[kMaxJC + 2];
     __shared__ uint32_t exf[kPlanBlock + 1];  // block-exclusive scan of full-chunk counts (+ total)
     __shared__ int64_t st_ae[kPlanBlock], st_s[kPlanBlock];
     __shared__ uint32_t st_m[kPlanBlock], st_flags[kPlanBlock], st_seed[kPlanBlock], st_slot[kPlanBlock];
+    __shared__ uint32_t s_total;
     const uint32_t ncols = plan_ncols(pg);
     for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) cursor[k] = hdr[kHdrBase + k];
     __syncthreads();
@@ -256,16 +261,17 @@ __global__ void __launch_bounds__(kPlanBlock) plan_emit_kernel(const uint64_t* _
         }
         const uint32_t slots = cursor[slot_col(pg)];
         cursor[slot_col(pg)] = 0;
-        if (blockIdx.x == 0) {
+        s_total = acc;
+        if (blockIdx.x == 0) {  // entry block 0, replica 0
             hdr[kHdrTotal] = acc;
             hdr[kHdrSlots] = slots;
             hdr[kHdrWork] = (uint32_t)((uint64_t)acc < capacity ? acc : capacity);
         }
     }
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) cursor[k] += blkoff[(uint64_t)k * gridDim.x + blockIdx.x];
+    for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) cursor[k] += blkoff[(uint64_t)k * neb + eb];
     __syncthreads();
-    const uint64_t i = (uint64_t)blockIdx.x * kPlanBlock + threadIdx.x;
+    const uint64_t i = (uint64_t)eb * kPlanBlock + threadIdx.x;
     EntryPlan p{};
     p.kind = 1;
     if (i < n) p = plan_entry(offsets[i], lengths[i], size, pg);
@@ -276,7 +282,7 @@ __global__ void __launch_bounds__(kPlanBlock) plan_emit_kernel(const uint64_t* _
     const uint32_t run0 = cursor[pg.jc];  // the block's first full-bin position (heads never move it)
     exf[threadIdx.x] = ex_full;
     if (threadIdx.x == 0) exf[kPlanBlock] = t_full;
-    if (i < n && !chunked) pslot[i] = kSerial;
+    if (rep == 0u && i < n && !chunked) pslot[i] = kSerial;
     if (chunked) {
         const uint32_t rs = run0 + ex_full;
         const uint32_t sb = cursor[slot_col(pg)] + ex_ps;
@@ -284,9 +290,9 @@ __global__ void __launch_bounds__(kPlanBlock) plan_emit_kernel(const uint64_t* _
         const uint32_t hpos = has_head ? atomicAdd(&cursor[p.jh], 1u) : 0u;
         const bool overflow = ((uint64_t)rs + p.full > capacity) || (has_head && (uint64_t)hpos >= capacity) ||
                               (p.ps && (uint64_t)sb + p.ps > capacity);
-        pslot[i] = overflow ? kDirect : (p.ps ? sb : kNoSlot);
         const uint32_t seed = seeds ? seeds[i] : seed_all;
-        if (has_head && (uint64_t)hpos < capacity)
+        if (rep == 0u) pslot[i] = overflow ? kDirect : (p.ps ? sb : kNoSlot);
+        if (rep == 0u && has_head && (uint64_t)hpos < capacity)
             descs[hpos] = overflow ? skip_desc() : chunk_desc(p, p.m - 1u, seed, (uint32_t)i, sb, pg);
         st_ae[threadIdx.x] = p.ae;
         st_s[threadIdx.x] = p.s;
@@ -296,7 +302,19 @@ __global__ void __launch_bounds__(kPlanBlock) plan_emit_kernel(const uint64_t* _
         st_slot[threadIdx.x] = sb;
     }
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k < t_full; k += kPlanBlock) {
+    // replicas split the full chunks only when nothing can overflow (total <= capacity): head
+    // positions come from LDS atomics whose order differs between replicas, and so could the
+    // overflow flags; otherwise replica 0 writes them all
+    uint32_t k0 = 0u, k1 = t_full;
+    if (reps > 1u) {
+        if ((uint64_t)s_total <= capacity) {
+            k0 = (uint32_t)((uint64_t)t_full * rep / reps);
+            k1 = (uint32_t)((uint64_t)t_full * (rep + 1u) / reps);
+        } else if (rep != 0u) {
+            k1 = 0u;
+        }
+    }
+    for (uint32_t k = k0 + threadIdx.x; k < k1; k += kPlanBlock) {
         // owner: the last thread t with exf[t] <= k (it has full chunks: exf[t + 1] > k)
         uint32_t lo = 0u, hi = kPlanBlock;
         while (hi - lo > 1u) {
@@ -311,7 +329,7 @@ __global__ void __launch_bounds__(kPlanBlock) plan_emit_kernel(const uint64_t* _
             if (pos < capacity) descs[pos] = skip_desc();
         } else {
             descs[pos] = chunk_desc_of(st_ae[t], st_s[t], st_m[t], fl & 0xFFu, (fl & 0x100u) != 0u, c, st_seed[t],
-                                       (uint32_t)((uint64_t)blockIdx.x * kPlanBlock + t), st_slot[t], pg);
+                                       (uint32_t)((uint64_t)eb * kPlanBlock + t), st_slot[t], pg);
         }
     }
 }
@@ -382,19 +400,23 @@ __global__ void __launch_bounds__(1024) plan_combine_kernel(
     const uint32_t* __restrict__ xtab, uint32_t xval, const uint32_t* __restrict__ x32tab,
     const uint32_t* __restrict__ btab, const uint32_t* __restrict__ xinv, uint32_t poly,
     const uint32_t* __restrict__ pslot, const uint32_t* __restrict__ partials, uint32_t* __restrict__ out,
-    uint32_t* __restrict__ err) {
+    uint32_t* __restrict__ err, uint32_t reps) {
+    // `reps` blocks per 1024-entry block (as plan_emit_kernel): each replica lists the block's
+    // entries of > kCombineSerial chunks and combines its share of them; replica 0 does the rest
+    // (invalid and serial entries are idempotent writes, cheap, and left to every replica)
+    const uint32_t eb = blockIdx.x / reps, rep = blockIdx.x - eb * reps;
     __shared__ uint32_t X[1024];
     __shared__ uint32_t W[1024];
     __shared__ uint32_t B[256];
     __shared__ uint32_t big[1024];
-    __shared__ uint32_t nbig;
+    __shared__ uint32_t wsum[kPlanBlock / 64 + 1];
     __shared__ uint32_t red[1024 / 64];
     for (int k = threadIdx.x; k < 1024; k += blockDim.x) X[k] = xtab[k];
     for (int k = threadIdx.x; k < 1024; k += blockDim.x) W[k] = x32tab[k];
     for (int k = threadIdx.x; k < 256; k += blockDim.x) B[k] = btab[k];
-    if (threadIdx.x == 0) nbig = 0u;
     __syncthreads();
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t i = (uint64_t)eb * blockDim.x + threadIdx.x;
+    uint32_t is_big = 0u;
     const uint32_t slot = i < n ? pslot[i] : kNoSlot;
     if (slot != kNoSlot && slot != kDirect) {
         const uint64_t o = offsets[i];
@@ -417,8 +439,8 @@ __global__ void __launch_bounds__(1024) plan_combine_kernel(
         } else {
             const EntryPlan p = plan_entry(o, l, size, pg);
             if (p.m > kCombineSerial) {
-                big[atomicAdd(&nbig, 1u)] = (uint32_t)threadIdx.x;
-            } else {
+                is_big = 1u;
+            } else if (rep == 0u) {
                 // partials in batches of 8 independent loads, then Horner from the head
                 uint32_t reg = partials[slot + p.m - 1u];
                 for (int c0 = (int)p.m - 2; c0 >= 0; c0 -= 8) {
@@ -435,13 +457,17 @@ __global__ void __launch_bounds__(1024) plan_combine_kernel(
             }
         }
     }
+    // the big-entry list in entry order (a scan, not LDS atomics): every replica must see the same
+    // list, since they split it by position
+    uint32_t nb;
+    const uint32_t bpos = block_excl_scan(is_big, wsum, nb);
+    if (is_big) big[bpos] = (uint32_t)threadIdx.x;
     __syncthreads();
-    const uint32_t nb = nbig;
     // 65 .. kCombineWave chunks: one wave per entry, the block's waves in parallel (4096 x 1 MiB
     // entries leave 4 blocks of 1024 such entries each; one entry at a time per block took 8 ms)
     const uint32_t lane = threadIdx.x & 63u, nwaves = blockDim.x >> 6;
-    for (uint32_t k = threadIdx.x >> 6; k < nb; k += nwaves) {
-        const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + big[k];
+    for (uint32_t k = rep * nwaves + (threadIdx.x >> 6); k < nb; k += reps * nwaves) {
+        const uint64_t e = (uint64_t)eb * blockDim.x + big[k];
         const EntryPlan p = plan_entry(offsets[e], lengths[e], size, pg);
         if (p.m > kCombineWave) continue;  // wave-uniform
         const uint32_t sl = pslot[e];
@@ -456,8 +482,8 @@ __global__ void __launch_bounds__(1024) plan_combine_kernel(
         if (lane == 0u) out[e] = ~(p.pad ? gf_mul_bits(xinv[p.pad], r, poly) : r);
     }
     // more chunks (entries of >= 16 MiB at 4 KiB chunks): the whole block per entry
-    for (uint32_t k = 0; k < nb; ++k) {
-        const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + big[k];
+    for (uint32_t k = rep; k < nb; k += reps) {
+        const uint64_t e = (uint64_t)eb * blockDim.x + big[k];
         const EntryPlan p = plan_entry(offsets[e], lengths[e], size, pg);
         if (p.m <= kCombineWave) continue;  // block-uniform
         const uint32_t sl = pslot[e];
