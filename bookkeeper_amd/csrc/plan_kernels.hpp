@@ -410,10 +410,12 @@ __global__ void __launch_bounds__(1024) plan_combine_kernel(
     __shared__ uint32_t B[256];
     __shared__ uint32_t big[1024];
     __shared__ uint32_t wsum[kPlanBlock / 64 + 1];
+    __shared__ uint32_t nbig;
     __shared__ uint32_t red[1024 / 64];
     for (int k = threadIdx.x; k < 1024; k += blockDim.x) X[k] = xtab[k];
     for (int k = threadIdx.x; k < 1024; k += blockDim.x) W[k] = x32tab[k];
     for (int k = threadIdx.x; k < 256; k += blockDim.x) B[k] = btab[k];
+    if (threadIdx.x == 0) nbig = 0u;
     __syncthreads();
     const uint64_t i = (uint64_t)eb * blockDim.x + threadIdx.x;
     uint32_t is_big = 0u;
@@ -440,6 +442,7 @@ __global__ void __launch_bounds__(1024) plan_combine_kernel(
             const EntryPlan p = plan_entry(o, l, size, pg);
             if (p.m > kCombineSerial) {
                 is_big = 1u;
+                if (reps == 1u) big[atomicAdd(&nbig, 1u)] = (uint32_t)threadIdx.x;
             } else if (rep == 0u) {
                 // partials in batches of 8 independent loads, then Horner from the head
                 uint32_t reg = partials[slot + p.m - 1u];
@@ -457,12 +460,17 @@ __global__ void __launch_bounds__(1024) plan_combine_kernel(
             }
         }
     }
-    // the big-entry list in entry order (a scan, not LDS atomics): every replica must see the same
-    // list, since they split it by position
+    // the big-entry list in entry order (a scan, not LDS atomics) when replicas must all see the same
+    // list, since they split it by position; a single replica keeps the cheaper LDS-atomic list
     uint32_t nb;
-    const uint32_t bpos = block_excl_scan(is_big, wsum, nb);
-    if (is_big) big[bpos] = (uint32_t)threadIdx.x;
-    __syncthreads();
+    if (reps > 1u) {  // kernel-uniform
+        const uint32_t bpos = block_excl_scan(is_big, wsum, nb);
+        if (is_big) big[bpos] = (uint32_t)threadIdx.x;
+        __syncthreads();
+    } else {
+        __syncthreads();
+        nb = nbig;
+    }
     // 65 .. kCombineWave chunks: one wave per entry, the block's waves in parallel (4096 x 1 MiB
     // entries leave 4 blocks of 1024 such entries each; one entry at a time per block took 8 ms)
     const uint32_t lane = threadIdx.x & 63u, nwaves = blockDim.x >> 6;
