@@ -1,6 +1,6 @@
 """Entry-size sweep (diagnostic, GPU box): device-resident uniform batches of 16 B .. 1 MiB entries
 through bkd_crc_batch_uniform (automatic lane choice, and every lane count), plus the same layout
-through the indexed path (chunked plan). ~4 GiB per batch. Prints one line per point; each
+through the indexed path (chunked plan, and the direct indexed kernel). ~4 GiB per batch. Prints one line per point; each
 configuration's output is checked against the first lane choice's."""
 import os
 import sys
@@ -55,6 +55,13 @@ def main():
         ck.set_plan_mode(0)
         assert torch.equal(out, ref), (L, "plan")
         print(f"{L:9d} {n:9d} {'plan':>10} {8:>5} {t * 1e3:8.3f} {n * L / t / GIB:8.1f} {n / t / 1e6:11.1f}",
+              flush=True)
+        # the direct indexed kernel (one entry per lane group, automatic lanes) on the same index
+        ck.set_plan_mode(1)
+        t = timed(lambda: ck.crc_batch(ck.CRC32C, base, offs, lens, out=out))
+        ck.set_plan_mode(0)
+        assert torch.equal(out, ref), (L, "direct")
+        print(f"{L:9d} {n:9d} {'direct':>10} {'auto':>5} {t * 1e3:8.3f} {n * L / t / GIB:8.1f} {n / t / 1e6:11.1f}",
               flush=True)
         del out, offs, lens
         torch.cuda.empty_cache()
