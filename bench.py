@@ -2,11 +2,12 @@
 """Headline benchmark: GiB/s CRC32C over batched 4 KiB ledger entries, device-resident.
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 launched by
-torch.distributed.run, one rank per GPU. A step = one launch of the digest engine over the
-whole per-GPU batch (BASELINE.json configs[1]: 1,048,576 x 4 KiB entries, CRC32C, seed 0,
-bytes = little-endian splitmix64 stream seed 42, generated on the device). Entries shard
-across ranks with no data-path collective (weak scaling); the only collectives are the
-timing barrier and the max-over-ranks reduction.
+torch.distributed.run, one rank per GPU (``--gpus N`` without that environment starts the N ranks
+itself, through torch.distributed.run, before anything touches a GPU). A step = one launch of the
+digest engine over the whole per-GPU batch (BASELINE.json configs[1]: 1,048,576 x 4 KiB entries,
+CRC32C, seed 0, bytes = little-endian splitmix64 stream seed 42, generated on the device). Entries
+shard across ranks with no data-path collective (weak scaling); the only collectives are the
+timing barriers, the max-over-ranks reduction and the gather of per-rank timings.
 
 Rank 0 prints ONE JSON line with ``roofline`` (dominant kernel, HIP-event timed on its own
 stream) and, at N=1, ``cpu_baseline`` (the reference's own circe crc32c() compiled from
@@ -17,6 +18,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -66,6 +69,35 @@ def shard_first_word(rank: int, entries_per_rank: int, entry_len: int) -> int:
     return rank * entries_per_rank * entry_len // 8
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(nprocs: int, argv: list[str]) -> int:
+    """``--gpus N`` outside torch.distributed.run: start the N ranks (one process per GPU) through
+    torch.distributed.run on 127.0.0.1 as child processes and return their exit code. Called before
+    anything in this process touches a GPU."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nprocs}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + argv
+    return subprocess.call(cmd)
+
+
+def gather_over_ranks(values: list[float], device=None) -> list[list[float]]:
+    """Every rank's timing values (all_gather of a few floats; timing only, never CRC data)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [list(values)]
+    t = torch.tensor(values, dtype=torch.float64, device=device)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [o.cpu().tolist() for o in out]
+
+
 def max_over_ranks(value: float, device=None) -> float:
     """Whole-job time = the slowest rank's (all_reduce MAX; the only cross-rank traffic)."""
     import torch
@@ -77,17 +109,33 @@ def max_over_ranks(value: float, device=None) -> float:
     return float(t.item())
 
 
-def cpu_baseline(host_sample: np.ndarray, entry_len: int, algo: int = 0, budget_s: float = 8.0):
-    """Reference circe crc32c() (oracle/_ref) over a bounded sample, all host cores we may use."""
-    import oracle
-    ref = oracle.ref()
-    n = host_sample.size // entry_len
-    out = np.zeros(n, dtype=np.uint32)
+def host_cores() -> tuple[int, str]:
+    """Every core this process may run on: the affinity mask, capped by a cgroup CPU quota when one
+    is set (a quota of Q cores makes more than Q threads time-slice, not run in parallel)."""
     try:
         cores = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
         cores = os.cpu_count() or 1
-    cores = max(1, min(16, cores))
+    why = f"sched_getaffinity: {cores}"
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            q = max(1, int(-(-int(quota) // int(period))))
+            if q < cores:
+                cores, why = q, f"{why}, cgroup cpu.max quota: {q}"
+    except (OSError, ValueError):
+        pass
+    return max(1, cores), why
+
+
+def cpu_baseline(host_sample: np.ndarray, entry_len: int, algo: int = 0, budget_s: float = 8.0):
+    """Reference circe crc32c() (oracle/_ref) over the sample on one core and on every host core
+    (all physical host cores)."""
+    import oracle
+    ref = oracle.ref()
+    n = host_sample.size // entry_len
+    out = np.zeros(n, dtype=np.uint32)
+    cores, cores_why = host_cores()
     u8p = host_sample.ctypes.data_as(oracle._u8p)
     o32 = out.ctypes.data_as(oracle._u32p)
     if ref is not None and algo == 0:
@@ -111,9 +159,10 @@ def cpu_baseline(host_sample: np.ndarray, entry_len: int, algo: int = 0, budget_
     t = run(cores, reps)
     value = host_sample.size * reps / t / GIB
     return {"value": round(value, 3), "unit": "GiB/s", "cores": cores, "kind": kind,
-            "single_core_value": round(one_core, 3), "cpu_model": _cpu_model(),
-            "sample": f"{n} x {entry_len} B entries of the same splitmix64 input ({host_sample.size / GIB:.3f} GiB), "
-                      f"{reps} passes over {cores} std::threads, one call per entry; {label}"}, out
+            "single_core_value": round(one_core, 3), "cpu_model": _cpu_model(), "cores_from": cores_why,
+            "sample": f"{n} x {entry_len} B entries of the same splitmix64 input ({host_sample.size / GIB:.3f} GiB, "
+                      f"the full config-1 batch when n = 1M), one pass on 1 core, then {reps} passes over {cores} "
+                      f"std::threads, one call per entry; {label}"}, out
 
 
 def cpu_baseline_indexed(host: np.ndarray, offs: np.ndarray, lens: np.ndarray, algo: int = 0, budget_s: float = 8.0):
@@ -121,11 +170,7 @@ def cpu_baseline_indexed(host: np.ndarray, offs: np.ndarray, lens: np.ndarray, a
     the reference's own circe crc32c() (oracle/_ref); CRC32: zlib's crc32(), the arithmetic
     java.util.zip.CRC32 runs (CRC32DigestManager.java:28-87)."""
     import oracle
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:  # pragma: no cover
-        cores = os.cpu_count() or 1
-    cores = max(1, min(16, cores))
+    cores, cores_why = host_cores()
     n = offs.size
     out = np.zeros(n, dtype=np.uint32)
     o64 = np.ascontiguousarray(offs, dtype=np.uint64)
@@ -154,7 +199,7 @@ def cpu_baseline_indexed(host: np.ndarray, offs: np.ndarray, lens: np.ndarray, a
     reps = max(1, int(budget_s / max(1e-6, t1 / cores)))
     t = run(cores, reps)
     return {"value": round(nbytes * reps / t / GIB, 3), "unit": "GiB/s", "cores": cores, "kind": kind,
-            "single_core_value": round(nbytes / t1 / GIB, 3), "cpu_model": _cpu_model(),
+            "single_core_value": round(nbytes / t1 / GIB, 3), "cpu_model": _cpu_model(), "cores_from": cores_why,
             "sample": f"the first {n} entries of the same Zipf index ({nbytes / GIB:.3f} GiB), {reps} passes over "
                       f"{cores} threads, one call per entry; {label}"}, out
 
@@ -224,6 +269,77 @@ def host_bench(args, ck, torch, rank) -> None:
            "digest_of_digests": int(np.bitwise_xor.reduce(out))}
     if rank == 0:
         print(json.dumps(res), flush=True)
+
+
+def digest_host_bench(args, ck, torch, rank, algo) -> None:
+    """Config 5's workload without a JVM: framed 4 KiB entries that live in HOST
+    memory as separate buffers (BatchedReadOp's ByteBufList, PendingAddOp's payloads), verified and
+    packaged through bkd_digest_verify_batch_host / bkd_digest_package_batch_host: gather into
+    pinned staging, H2D, the device sequence, D2H of statuses/frames. PCIe-inclusive, end to end."""
+    import ctypes
+    from bookkeeper_amd import digest as dg
+    from bookkeeper_amd._native import check, lib
+    n = args.entries or (1 << 20)
+    L = 4096
+    dm = dg.DigestManager.instantiate(7, b"", dg.DigestType.CRC32C if algo == ck.CRC32C else dg.DigestType.CRC32)
+    mac = dm.macCodeLength
+    plen = L - 32 - mac
+    dev_tmp = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    ck.fill_splitmix64(dev_tmp, 42)
+    host = np.ascontiguousarray(dev_tmp.cpu().numpy())  # pageable host memory, like Netty direct buffers
+    del dev_tmp
+    ids = np.arange(n, dtype=np.int64)
+    lacs = ids - 1
+    lf = np.full(n, plen, dtype=np.int64)
+    base = host.ctypes.data
+    pay_ptrs = (base + ids.astype(np.uint64) * L + 32 + mac).astype(np.uint64)
+    pay_lens = np.full(n, plen, dtype=np.uint32)
+    hdrs = np.zeros((n, 32 + mac), dtype=np.uint8)
+    digests = np.zeros(n, dtype=np.uint32)
+    vp = ctypes.c_void_p
+
+    def package():
+        check(lib().bkd_digest_package_batch_host(algo, dm.ledgerId, vp(ids.ctypes.data), vp(lacs.ctypes.data),
+                                                  vp(lf.ctypes.data), vp(pay_ptrs.ctypes.data),
+                                                  vp(pay_lens.ctypes.data), n, vp(hdrs.ctypes.data), 32 + mac,
+                                                  vp(digests.ctypes.data)))
+    package()
+    host.reshape(n, L)[:, :32 + mac] = hdrs  # frames = [header][digest][payload], each its own 4 KiB buffer
+    frame_ptrs = (base + ids.astype(np.uint64) * L).astype(np.uint64)
+    frame_lens = np.full(n, L, dtype=np.uint32)
+    status = np.zeros(n, dtype=np.int32)
+    first_bad = ctypes.c_uint64(0)
+
+    def verify():
+        check(lib().bkd_digest_verify_batch_host(algo, dm.ledgerId, 0, 0, vp(frame_ptrs.ctypes.data),
+                                                 vp(frame_lens.ctypes.data), n, vp(status.ctypes.data),
+                                                 ctypes.byref(first_bad)))
+
+    def timed(fn):
+        for _ in range(max(1, min(args.warmup, 2))):
+            fn()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            fn()
+        return (time.perf_counter() - t0) / args.steps
+    steps = args.steps
+    t_verify = timed(verify)
+    ok = bool((status == 0).all()) and first_bad.value == n
+    t_pack = timed(package)
+    res = {"metric": "GiB/s framed 4 KiB ledger entries in host memory, batched DigestManager verify incl. "
+                     "gather + PCIe H2D/D2H (end to end; config 5's workload, not the headline)",
+           "value": round(n * L / t_verify / GIB, 2), "unit": "GiB/s", "n_gpus": 1, "steps": steps,
+           "warmup": args.warmup, "ms_per_step": round(t_verify * 1e3, 3), "higher_is_better": True, "dtype": "u8",
+           "data": "synthetic (splitmix64, seed 42), pageable host memory, one 4 KiB buffer per entry",
+           "config": {"workload": f"{n} framed entries x {L} B ({args.algo}) as separate host buffers "
+                                  f"(ByteBufList), 64 MiB double-buffered segments"},
+           "all_verified": ok, "entries_per_s": round(n / t_verify, 0),
+           "package": {"GiB_s_payload": round(n * plen / t_pack / GIB, 2), "ms": round(t_pack * 1e3, 3),
+                       "entries_per_s": round(n / t_pack, 0)}}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if not ok:
+        raise SystemExit("VERIFY FAILURE: host-resident entries did not verify")
 
 
 def digest_bench(args, ck, torch, rank, dev, stream, algo) -> None:
@@ -296,7 +412,8 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--config", default="uniform4k", choices=["uniform4k", "shard8m", "zipf", "indexed4k", "host4k", "verify4k"])
+    ap.add_argument("--config", default="uniform4k",
+                    choices=["uniform4k", "shard8m", "zipf", "indexed4k", "host4k", "verify4k", "verify4k_host"])
     ap.add_argument("--algo", default="crc32c", choices=["crc32c", "crc32"])
     ap.add_argument("--entries", type=int, default=0, help="entries per GPU (default by config)")
     ap.add_argument("--lanes", type=int, default=0, help="force lanes per entry group (0 = auto)")
@@ -309,6 +426,8 @@ def main() -> None:
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL) on a real node; gloo only to rehearse several ranks on one GPU")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(self_launch(args.gpus, sys.argv[1:]))
 
     import torch
     import torch.distributed as dist
@@ -340,6 +459,8 @@ def main() -> None:
         return host_bench(args, ck, torch, rank)
     if args.config == "verify4k":
         return digest_bench(args, ck, torch, rank, dev, stream, algo)
+    if args.config == "verify4k_host":
+        return digest_host_bench(args, ck, torch, rank, algo)
     if args.config in ("uniform4k", "shard8m"):
         entry_len = 4096
         n = args.entries or (1 << 20 if args.config == "uniform4k" else 8 << 20)
@@ -383,6 +504,21 @@ def main() -> None:
         step()
     torch.cuda.synchronize()
 
+    solo_kernel_s = None
+    if world > 1:  # each rank alone on the node, in turn: the same-run 1-GPU rate per rank
+        for r in range(world):
+            dist.barrier()
+            if r == rank:
+                s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                solo_steps = max(5, min(args.steps, 20))
+                s0.record(stream)
+                for _ in range(solo_steps):
+                    step()
+                s1.record(stream)
+                torch.cuda.synchronize()
+                solo_kernel_s = s0.elapsed_time(s1) / 1e3 / solo_steps
+            dist.barrier()
+
     # HIP events on the launch stream bracket the K back-to-back launches (no event packets between
     # launches); the average launch duration is their span / K
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -400,7 +536,9 @@ def main() -> None:
     elapsed = time.perf_counter() - t0
     avg_kernel_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
 
-    elapsed_max = max_over_ranks(elapsed, dev if args.dist_backend == "nccl" else None)
+    coll_dev = dev if args.dist_backend == "nccl" else None
+    elapsed_max = max_over_ranks(elapsed, coll_dev)
+    per_rank = gather_over_ranks([elapsed, avg_kernel_s, solo_kernel_s or avg_kernel_s], coll_dev)
 
     total_payload = payload_bytes * world * args.steps  # every rank processes its batch once per step
     value = total_payload / elapsed_max / GIB
@@ -426,11 +564,20 @@ def main() -> None:
                      "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic(args.config),
                      "kernel": kernel_name, "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
                      "algorithmic_bytes_per_launch": algo_bytes},
+        # per GPU: its own wall rate over the timed region, its kernel time, and (N > 1) its rate when
+        # it ran alone on the node in this same run; efficiency = (aggregate / N) / mean solo rate
+        "per_gpu": [{"rank": r, "GiB_s": round(payload_bytes * args.steps / e / GIB, 2),
+                     "kernel_ms": round(k * 1e3, 4), "solo_GiB_s": round(payload_bytes / so / GIB, 2)}
+                    for r, (e, k, so) in enumerate(per_rank)],
+        "per_gpu_GiB_s": round(value / world, 2),
     }
+    if world > 1:
+        solo_mean = float(np.mean([payload_bytes / so / GIB for _, _, so in per_rank]))
+        result["efficiency_vs_solo"] = round(value / world / solo_mean, 4)
     if args.config == "zipf" and world == 1 and not args.no_buckets:
         result["buckets"] = bucket_rates(ck, torch, algo, base, offs, lens, stream, max(3, args.steps))
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "zipf":
-        m = min(n, 65536)  # ~0.4 GiB of the same packed buffer
+        m = n  # the whole packed batch (6.3 GiB for config 3): well past any cache
         span = int(offs[m - 1] + lens[m - 1])
         host = np.ascontiguousarray(base[:span].cpu().numpy())
         result["cpu_baseline"], want = cpu_baseline_indexed(host, offs[:m], lens[:m], algo)
@@ -442,7 +589,7 @@ def main() -> None:
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in ("uniform4k", "shard8m"):
         # cpu_baseline leg: the reference timed on the host cores over a bounded sample; its
         # digests for that sample double as a parity spot check of the GPU output.
-        m = min(n, 65536)
+        m = min(n, 1 << 20)  # config 1's full 1M x 4 KiB (4 GiB)
         host = np.ascontiguousarray(base[: m * entry_len].cpu().numpy())
         result["cpu_baseline"], want = cpu_baseline(host, entry_len, algo)
         got = out[:m].cpu().numpy().view(np.uint32)

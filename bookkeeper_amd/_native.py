@@ -1,8 +1,10 @@
 """ctypes binding of libbkdigest.so (include/bkdigest.h).
 
-There is deliberately no fallback: if the HIP library is missing or no GPU is visible,
-every compute call raises. The reference's CPU providers (JNI SSE4.2 / Java9 / Java8,
-Crc32cIntChecksum.java:28-36) stay the caller's business, never a silent substitute here.
+There is deliberately no Python fallback: if the library is missing, every call raises
+NativeUnavailable. Inside the library, batch calls always run on the GPU (BKD_ERR_NO_DEVICE
+without one); only the per-call host-buffer resume has the library's own native CPU route
+(host_crc.cpp), the role the reference's JNI SSE4.2 provider plays in its selection chain
+(Crc32cIntChecksum.java:28-36).
 """
 from __future__ import annotations
 
@@ -57,6 +59,17 @@ PROTOTYPES = {
     "bkd_stream_sync": (_int, [_vp]),
     "bkd_crc_batch_host": (_int, [_int, _vp, _u64, _vp, _vp, _u64, _vp, _u32, _vp]),
     "bkd_resume": (_int, [_int, _u32, _vp, _u64, _c.POINTER(_u32)]),
+    "bkd_resume_host": (_int, [_int, _u32, _vp, _u64, _c.POINTER(_u32)]),
+    "bkd_resume_device": (_int, [_int, _u32, _vp, _u64, _vp, _c.POINTER(_u32)]),
+    "bkd_cpu_resume": (_int, [_int, _u32, _vp, _u64, _c.POINTER(_u32)]),
+    "bkd_set_cpu_route_max": (_int, [_u64]),
+    "bkd_get_cpu_route_max": (_u64, []),
+    "bkd_cpu_impl": (_c.c_char_p, []),
+    "bkd_circe_supported": (_int, []),
+    "bkd_circe_alloc_config": (_i64, [_vp, _c.c_int32]),
+    "bkd_circe_free_config": (None, [_i64]),
+    "bkd_digest_verify_batch_host": (_int, [_int, _i64, _i64, _int, _vp, _vp, _u64, _vp, _vp]),
+    "bkd_digest_package_batch_host": (_int, [_int, _i64, _vp, _vp, _vp, _vp, _vp, _u64, _vp, _u64, _vp]),
     "bkd_digest_package_batch": (_int, [_int, _i64, _vp, _vp, _vp, _vp, _u64, _vp, _vp, _u64, _vp, _u64, _vp, _vp]),
     "bkd_digest_verify_batch": (_int, [_int, _i64, _i64, _int, _vp, _u64, _vp, _vp, _u64, _vp, _vp, _vp]),
     "bkd_entrylog_index": (_int, [_vp, _u64, _u64, _vp, _vp, _vp, _u64, _vp, _vp]),

@@ -14,8 +14,9 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libbkdigest.so")
 SOURCES = [os.path.join(CSRC, "bkdigest.hip")]
-DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("crc_kernels.hpp", "crc_tables.hpp", "plan_kernels.hpp")] + [
-    os.path.join(ROOT, "include", "bkdigest.h")]
+HOST_SOURCES = [os.path.join(CSRC, "host_crc.cpp")]  # CPU route (plain C++, built with the host compiler)
+DEPS = SOURCES + HOST_SOURCES + [os.path.join(CSRC, f) for f in (
+    "crc_kernels.hpp", "crc_tables.hpp", "plan_kernels.hpp", "host_crc.hpp")] + [os.path.join(ROOT, "include", "bkdigest.h")]
 ARCH = os.environ.get("BKD_OFFLOAD_ARCH", "gfx950")
 
 
@@ -24,6 +25,13 @@ def hipcc() -> str:
         if cand and os.path.exists(cand):
             return cand
     raise RuntimeError("hipcc not found: cannot build libbkdigest.so")
+
+
+def cxx() -> str:
+    for cand in (os.environ.get("CXX"), shutil.which("g++"), shutil.which("c++")):
+        if cand and shutil.which(cand):
+            return cand
+    return hipcc()
 
 
 def needs_build() -> bool:
@@ -37,9 +45,19 @@ def build_native(force: bool = False, extra_flags: list[str] | None = None, out:
     out = out or LIB
     if not force and out == LIB and not needs_build():
         return out
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-I", os.path.join(ROOT, "include"), "-o", out + ".tmp"] + SOURCES + list(extra_flags or [])
-    subprocess.run(cmd, check=True)
+    objs = []
+    for src in HOST_SOURCES:
+        obj = os.path.join(CSRC, os.path.splitext(os.path.basename(src))[0] + f"_{os.getpid()}.o")
+        subprocess.run([cxx(), "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-c", src, "-o", obj], check=True)
+        objs.append(obj)
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden",
+           "-I", os.path.join(ROOT, "include"), "-o", out + ".tmp"] + objs + SOURCES + ["-lpthread"] + list(
+        extra_flags or [])
+    try:
+        subprocess.run(cmd, check=True)
+    finally:
+        for obj in objs:
+            os.remove(obj)
     os.replace(out + ".tmp", out)
     return out
 

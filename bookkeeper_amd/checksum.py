@@ -15,10 +15,14 @@ the reference returns; the batch API returns uint32 arrays.
 
 Buffers: ``bytes``/``bytearray``/``memoryview``/numpy arrays are host buffers (the reference's
 ``byte[]`` / direct ``ByteBuf``); ``torch`` tensors on a HIP device are device-resident buffers
-(the new batch path). There is no CPU arithmetic in this module.
+(the new batch path). There is no CPU arithmetic in this module: host buffers go to
+``bkd_resume_host`` (the library's native CPU route for small buffers or without a device, the
+GPU above ``cpu_route_max``), device tensors to ``bkd_resume_device`` on the tensor's current
+stream, so a resume is ordered after the kernels that wrote the tensor.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 
 import numpy as np
@@ -27,7 +31,7 @@ from . import _native
 from ._native import CRC32, CRC32C, check, lib
 
 __all__ = ["CRC32C", "CRC32", "GpuIntHash", "Crc32cIntChecksum", "crc_batch", "crc_batch_uniform",
-           "crc_batch_segments", "crc_batch_host", "to_java_int"]
+           "crc_batch_segments", "crc_batch_host", "cpu_resume", "set_cpu_route_max", "to_java_int"]
 
 
 def to_java_int(v: int) -> int:
@@ -40,12 +44,27 @@ def _is_torch_tensor(x) -> bool:
 
 
 def _stream_ptr(stream, tensor=None):
+    """The HIP stream a call is enqueued on: `stream` if given (a torch.cuda.Stream on the tensor's
+    device, or a raw handle), else the tensor device's current stream. The library runs the call on
+    that stream's device; for the null stream, on the current device, which _on_device sets."""
     if stream is not None:
+        sdev = getattr(stream, "device", None)
+        if sdev is not None and tensor is not None and _is_torch_tensor(tensor) and tensor.is_cuda \
+                and sdev != tensor.device:
+            raise ValueError(f"stream is on {sdev} but the buffer is on {tensor.device}")
         return ctypes.c_void_p(int(getattr(stream, "cuda_stream", stream)))
     if tensor is not None and _is_torch_tensor(tensor) and tensor.is_cuda:
         import torch
         return ctypes.c_void_p(int(torch.cuda.current_stream(tensor.device).cuda_stream))
     return ctypes.c_void_p(0)
+
+
+def _on_device(tensor):
+    """Makes the tensor's device current for the call (the null stream runs on the current device)."""
+    if _is_torch_tensor(tensor) and tensor.is_cuda:
+        import torch
+        return torch.cuda.device(tensor.device)
+    return contextlib.nullcontext()
 
 
 def _host_view(buf) -> np.ndarray:
@@ -83,16 +102,19 @@ class GpuIntHash:
                 raise IndexError("range outside buffer")  # AbstractIncrementalIntHash.java:66-67
             if not buffer.is_contiguous():
                 raise ValueError("device buffer must be contiguous")
+            if not buffer.is_cuda:  # a CPU tensor is a host buffer
+                return self.resume(current, buffer.numpy(), offset, length)
             ptr = ctypes.c_void_p(buffer.data_ptr() + offset)
-            keep = buffer
+            with _on_device(buffer):
+                check(lib().bkd_resume_device(self.algo, current & 0xFFFFFFFF, ptr, length,
+                                              _stream_ptr(None, buffer), ctypes.byref(out)))
         else:
             view = _host_view(buffer)
             if offset < 0 or offset + length > view.size:
                 raise IndexError("range outside buffer")
-            keep = view
             ptr = ctypes.c_void_p(view.ctypes.data + offset) if view.size else ctypes.c_void_p(0)
-        check(lib().bkd_resume(self.algo, current & 0xFFFFFFFF, ptr, length, ctypes.byref(out)))
-        del keep
+            check(lib().bkd_resume_host(self.algo, current & 0xFFFFFFFF, ptr, length, ctypes.byref(out)))
+            del view
         return to_java_int(out.value)
 
     # IntHash.acceptsMemoryAddressBuffer (IntHash.java:34; JniIntHash.java:60-63)
@@ -105,7 +127,10 @@ class GpuIntHash:
 
 
 class Crc32cIntChecksum:
-    """Static facade (Crc32cIntChecksum.java:24-100) with the GPU provider selected."""
+    """Static facade (Crc32cIntChecksum.java:24-100). The reference selects its provider once at class
+    init and never throws (:28-36); here the one provider is libbkdigest.so, whose host-buffer resume
+    has its own CPU route, so a missing GPU is not an error. A missing library is (NativeUnavailable):
+    it is the product, and nothing here substitutes Python arithmetic for it."""
 
     _hash: GpuIntHash | None = None
 
@@ -133,17 +158,29 @@ class Crc32cIntChecksum:
 # Device-resident batch API (torch tensors on a HIP device)
 # ---------------------------------------------------------------------------------------------
 
-def _dev_ptr(t, name: str, dtype=None):
-    import torch
+def _dev_ptr(t, name: str, dtype=None, device=None, min_numel: int | None = None):
+    """Device pointer of a contiguous tensor, checked: on `device` (the base buffer's), of `dtype`
+    (a dtype or a tuple of allowed dtypes) and with at least `min_numel` elements."""
     if t is None:
         return ctypes.c_void_p(0)
     if not (_is_torch_tensor(t) and t.is_cuda):
         raise TypeError(f"{name} must be a torch tensor on a HIP device")
-    if dtype is not None and t.dtype != dtype:
-        raise TypeError(f"{name} must have dtype {dtype}")
+    if dtype is not None:
+        allowed = dtype if isinstance(dtype, tuple) else (dtype,)
+        if t.dtype not in allowed:
+            raise TypeError(f"{name} must have dtype {' or '.join(str(d) for d in allowed)}, not {t.dtype}")
+    if device is not None and t.device != device:
+        raise ValueError(f"{name} is on {t.device} but the base buffer is on {device}")
+    if min_numel is not None and t.numel() < min_numel:
+        raise ValueError(f"{name} has {t.numel()} elements, needs {min_numel}")
     if not t.is_contiguous():
         raise ValueError(f"{name} must be contiguous")
     return ctypes.c_void_p(t.data_ptr())
+
+
+def _u32_dtypes():
+    import torch
+    return (torch.int32, torch.uint32) if hasattr(torch, "uint32") else (torch.int32,)
 
 
 def crc_batch_uniform(algo: int, base, entry_len: int, n: int, stride: int | None = None, seeds=None,
@@ -156,11 +193,11 @@ def crc_batch_uniform(algo: int, base, entry_len: int, n: int, stride: int | Non
         raise IndexError("uniform batch exceeds base buffer")
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=base.device)
-    if seeds is not None and seeds.numel() < n:
-        raise ValueError("seeds shorter than n")
-    check(lib().bkd_crc_batch_uniform(algo, _dev_ptr(base, "base"), stride, entry_len, n,
-                                      _dev_ptr(seeds, "seeds"), seed_all & 0xFFFFFFFF, _dev_ptr(out, "out"),
-                                      _stream_ptr(stream, base)))
+    u32, dev = _u32_dtypes(), base.device
+    with _on_device(base):
+        check(lib().bkd_crc_batch_uniform(algo, _dev_ptr(base, "base"), stride, entry_len, n,
+                                          _dev_ptr(seeds, "seeds", u32, dev, n), seed_all & 0xFFFFFFFF,
+                                          _dev_ptr(out, "out", u32, dev, n), _stream_ptr(stream, base)))
     return out
 
 
@@ -178,12 +215,14 @@ def crc_batch(algo: int, base, offsets, lengths, seeds=None, seed_all: int = 0, 
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=base.device)
     nbytes = base.numel() * base.element_size()
-    st = _stream_ptr(stream, base)
-    check(lib().bkd_crc_batch(algo, _dev_ptr(base, "base"), nbytes, _dev_ptr(offsets, "offsets", torch.int64),
-                              _dev_ptr(lengths, "lengths", torch.int32), n, _dev_ptr(seeds, "seeds"),
-                              seed_all & 0xFFFFFFFF, _dev_ptr(out, "out"), st))
-    if sync_check:
-        check(lib().bkd_stream_sync(st))
+    u32, dev = _u32_dtypes(), base.device
+    with _on_device(base):
+        st = _stream_ptr(stream, base)
+        check(lib().bkd_crc_batch(algo, _dev_ptr(base, "base"), nbytes, _dev_ptr(offsets, "offsets", torch.int64, dev),
+                                  _dev_ptr(lengths, "lengths", u32, dev), n, _dev_ptr(seeds, "seeds", u32, dev, n),
+                                  seed_all & 0xFFFFFFFF, _dev_ptr(out, "out", u32, dev, n), st))
+        if sync_check:
+            check(lib().bkd_stream_sync(st))
     return out
 
 
@@ -202,14 +241,17 @@ def crc_batch_segments(algo: int, base, seg_offsets, seg_lengths, seg_first, see
         raise ValueError("seg_offsets/seg_lengths size mismatch")
     if out is None:
         out = torch.empty(max(n, 0), dtype=torch.int32, device=base.device)
-    st = _stream_ptr(stream, base)
-    check(lib().bkd_crc_batch_segments(algo, _dev_ptr(base, "base"), base.numel() * base.element_size(),
-                                       _dev_ptr(seg_offsets, "seg_offsets", torch.int64),
-                                       _dev_ptr(seg_lengths, "seg_lengths", torch.int32), nseg,
-                                       _dev_ptr(seg_first, "seg_first", torch.int64), n, _dev_ptr(seeds, "seeds"),
-                                       seed_all & 0xFFFFFFFF, _dev_ptr(out, "out"), st))
-    if sync_check:
-        check(lib().bkd_stream_sync(st))
+    u32, dev = _u32_dtypes(), base.device
+    with _on_device(base):
+        st = _stream_ptr(stream, base)
+        check(lib().bkd_crc_batch_segments(algo, _dev_ptr(base, "base"), base.numel() * base.element_size(),
+                                           _dev_ptr(seg_offsets, "seg_offsets", torch.int64, dev),
+                                           _dev_ptr(seg_lengths, "seg_lengths", u32, dev), nseg,
+                                           _dev_ptr(seg_first, "seg_first", torch.int64, dev), n,
+                                           _dev_ptr(seeds, "seeds", u32, dev, n), seed_all & 0xFFFFFFFF,
+                                           _dev_ptr(out, "out", u32, dev, n), st))
+        if sync_check:
+            check(lib().bkd_stream_sync(st))
     return out
 
 
@@ -233,8 +275,31 @@ def crc_batch_host(algo: int, base, offsets, lengths, seeds=None, seed_all: int 
 def fill_splitmix64(buf, seed: int, first_word: int = 0, stream=None) -> None:
     """Device-side synthetic input: little-endian splitmix64 words."""
     nbytes = buf.numel() * buf.element_size()
-    check(lib().bkd_fill_splitmix64(_dev_ptr(buf, "buf"), nbytes, seed & (2**64 - 1), first_word,
-                                    _stream_ptr(stream, buf)))
+    with _on_device(buf):
+        check(lib().bkd_fill_splitmix64(_dev_ptr(buf, "buf"), nbytes, seed & (2**64 - 1), first_word,
+                                        _stream_ptr(stream, buf)))
+
+
+def cpu_resume(algo: int, current: int, buffer) -> int:
+    """The library's CPU route only (bkd_cpu_resume), whatever the size; Java int bit pattern."""
+    view = _host_view(buffer)
+    out = ctypes.c_uint32(0)
+    check(lib().bkd_cpu_resume(algo, current & 0xFFFFFFFF, ctypes.c_void_p(view.ctypes.data if view.size else 0),
+                               view.size, ctypes.byref(out)))
+    return to_java_int(out.value)
+
+
+def set_cpu_route_max(nbytes: int) -> None:
+    """Host buffers up to nbytes take the CPU route in per-call resumes (0 = GPU whenever present)."""
+    check(lib().bkd_set_cpu_route_max(nbytes))
+
+
+def get_cpu_route_max() -> int:
+    return int(lib().bkd_get_cpu_route_max())
+
+
+def cpu_impl() -> str:
+    return lib().bkd_cpu_impl().decode()
 
 
 def set_group_lanes(lanes: int) -> None:

@@ -1,24 +1,30 @@
 // libbkdigest.so — C-ABI over the CDNA4 CRC kernels (include/bkdigest.h).
 //
-// Runtime glue only: per-device operator-table images, launch geometry, bounds flags,
-// the host-memory staging path and the DigestManager batch framing sequence. No CPU
-// compute path exists here: without a device every entry point returns BKD_ERR_NO_DEVICE.
+// Runtime glue: per-device operator-table images, launch geometry, per-stream bounds flags,
+// the host-memory staging paths and the DigestManager batch framing sequences. The only CPU
+// arithmetic is the per-call route for host buffers (host_crc.cpp, bkd_resume*); every batch
+// entry point runs on the GPU and returns BKD_ERR_NO_DEVICE without one.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
+#include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/bkdigest.h"
 #include "crc_kernels.hpp"
 #include "plan_kernels.hpp"
 #include "crc_tables.hpp"
+#include "host_crc.hpp"
 
 namespace {
 
@@ -54,6 +60,24 @@ struct StreamScratch {
     std::recursive_mutex mu;
     uint8_t* buf[3] = {};  // slot 0: plan scratch (launch_plan), 1: verify pipeline, 2: segment CRCs
     size_t cap[3] = {};
+    // Sticky bounds-violation flag of the indexed batches enqueued on this stream (one per
+    // stream, so a caller's out-of-range entry is reported to that caller's bkd_stream_sync
+    // only); read and cleared in stream order. h_err: pinned landing word for the read.
+    uint32_t* err = nullptr;
+    uint32_t* h_err = nullptr;
+    hipError_t flag(hipStream_t st, uint32_t** out) {
+        if (!err) {
+            hipError_t e = hipMallocAsync((void**)&err, sizeof(uint32_t), st);
+            if (e == hipSuccess) e = hipMemsetAsync(err, 0, sizeof(uint32_t), st);
+            if (e == hipSuccess && !h_err) e = hipHostMalloc((void**)&h_err, sizeof(uint32_t), hipHostMallocDefault);
+            if (e != hipSuccess) {
+                err = nullptr;
+                return e;
+            }
+        }
+        *out = err;
+        return hipSuccess;
+    }
     // Returns slot `which` with at least `bytes` bytes, stream-ordered on `st`.
     hipError_t get(int which, size_t bytes, hipStream_t st, uint8_t** out) {
         if (cap[which] < bytes) {
@@ -89,7 +113,6 @@ struct DeviceState {
     bool ready = false;
     int cus = 0;
     uint32_t* tables[2][kNumLaneChoices] = {};  // [algo][lane choice] compact operator images
-    uint32_t* err = nullptr;      // sticky bounds-violation flag for indexed batches
     uint32_t* xinv[2] = {};       // [algo] x^(-8k), k = 0..127: removes the plan's zero padding
     std::map<uint64_t, uint32_t*> xtab;  // (algo, CH) -> x^(8*CH) operator for the plan's combine
     std::map<hipStream_t, std::unique_ptr<StreamScratch>> scratch;
@@ -109,13 +132,41 @@ std::atomic<int> g_plan_pf{2};  // loads in flight per lane in the chunk kernel 
 // Indexed batches whose base buffer is at most this size skip the plan (latency over balance).
 constexpr uint64_t kDirectMaxBytes = 256u << 10;
 
-int current_device(int* dev) {
-    int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return fail(BKD_ERR_NO_DEVICE, "no HIP device");
-    BKD_HIP(hipGetDevice(dev));
+// Visible HIP devices, probed once per process (0 when the runtime finds none).
+int visible_devices() {
+    static std::once_flag once;
+    static int count = 0;
+    std::call_once(once, [] {
+        if (hipGetDeviceCount(&count) != hipSuccess) {
+            (void)hipGetLastError();
+            count = 0;
+        }
+    });
+    return count;
+}
+
+// The device a call runs on: a created stream's own device (hipStreamGetDevice), else the
+// calling thread's current device (null, legacy and per-thread default streams).
+int stream_device(hipStream_t st, int* dev) {
+    if (visible_devices() <= 0) return fail(BKD_ERR_NO_DEVICE, "no HIP device");
+    if (st == nullptr || st == hipStreamLegacy || st == hipStreamPerThread) {
+        BKD_HIP(hipGetDevice(dev));
+    } else {
+        hipDevice_t d = 0;
+        BKD_HIP(hipStreamGetDevice(st, &d));
+        *dev = (int)d;
+    }
     if (*dev < 0 || *dev >= kMaxDevices) return fail(BKD_ERR_NO_DEVICE, "device index out of range");
     return BKD_OK;
 }
+
+// Makes the stream's device current for the duration of a call and restores the caller's.
+struct DeviceScope {
+    int prev = -1;
+    ~DeviceScope() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
 
 int init_device_locked(int dev) {
     DeviceState& ds = g_dev[dev];
@@ -148,8 +199,6 @@ int init_device_locked(int dev) {
         uint64_t thr = UINT64_MAX;
         (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
     }
-    BKD_HIP(hipMalloc(&ds.err, sizeof(uint32_t)));
-    BKD_HIP(hipMemset(ds.err, 0, sizeof(uint32_t)));
     BKD_HIP(hipSetDevice(prev));
     ds.ready = true;
     return BKD_OK;
@@ -172,10 +221,16 @@ int xtab_for(DeviceState& ds, int algo, uint32_t ch, const uint32_t** out) {
     return BKD_OK;
 }
 
-int ensure_current(DeviceState** out) {
+int enter(hipStream_t st, DeviceScope& scope, DeviceState** out) {
     int dev = 0;
-    int rc = current_device(&dev);
+    int rc = stream_device(st, &dev);
     if (rc) return rc;
+    int cur = 0;
+    BKD_HIP(hipGetDevice(&cur));
+    if (cur != dev) {
+        BKD_HIP(hipSetDevice(dev));
+        scope.prev = cur;
+    }
     {
         std::lock_guard<std::mutex> lk(g_mu);
         rc = init_device_locked(dev);
@@ -216,14 +271,14 @@ constexpr bool kNT = BKD_NT != 0;
 
 template <int G, class Src>
 int launch_groups(DeviceState& ds, int algo, const uint8_t* base, const Src& src, uint64_t host_count,
-                  hipStream_t stream) {
+                  hipStream_t stream, uint32_t* err) {
     if (host_count == 0) return BKD_OK;
     const uint64_t groups_per_block = bkd::kBlock / G;
     uint64_t blocks = (host_count + groups_per_block - 1) / groups_per_block;
     blocks = std::min<uint64_t>(blocks, (uint64_t)ds.cus);
     const uint32_t* tab = ds.tables[algo][lane_index(G)];
     hipLaunchKernelGGL((bkd::crc_groups_kernel<G, kPF, kNT, Src>), dim3((unsigned)blocks), dim3(bkd::kBlock), 0,
-                       stream, base, src, tab, ds.err);
+                       stream, base, src, tab, err);
     BKD_HIP(hipGetLastError());
     return BKD_OK;
 }
@@ -231,14 +286,14 @@ int launch_groups(DeviceState& ds, int algo, const uint8_t* base, const Src& src
 // host_count: an upper bound of src.count() used only to size the grid.
 template <class Src>
 int dispatch_lanes(DeviceState& ds, int lanes, int algo, const uint8_t* base, const Src& src, uint64_t host_count,
-                   hipStream_t stream) {
+                   hipStream_t stream, uint32_t* err = nullptr) {
     switch (lanes) {
-        case 1: return launch_groups<1>(ds, algo, base, src, host_count, stream);
-        case 4: return launch_groups<4>(ds, algo, base, src, host_count, stream);
-        case 8: return launch_groups<8>(ds, algo, base, src, host_count, stream);
-        case 16: return launch_groups<16>(ds, algo, base, src, host_count, stream);
-        case 32: return launch_groups<32>(ds, algo, base, src, host_count, stream);
-        case 64: return launch_groups<64>(ds, algo, base, src, host_count, stream);
+        case 1: return launch_groups<1>(ds, algo, base, src, host_count, stream, err);
+        case 4: return launch_groups<4>(ds, algo, base, src, host_count, stream, err);
+        case 8: return launch_groups<8>(ds, algo, base, src, host_count, stream, err);
+        case 16: return launch_groups<16>(ds, algo, base, src, host_count, stream, err);
+        case 32: return launch_groups<32>(ds, algo, base, src, host_count, stream, err);
+        case 64: return launch_groups<64>(ds, algo, base, src, host_count, stream, err);
         default: return fail(BKD_ERR_INVALID_ARG, "lanes must be 1, 4, 8, 16, 32 or 64");
     }
 }
@@ -290,7 +345,9 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     StreamScratch& sc = scratch_for(ds, st);
     std::lock_guard<std::recursive_mutex> lk(sc.mu);
     uint8_t* sb = nullptr;
+    uint32_t* err = nullptr;
     hipError_t e = sc.get(0, cv.used, st, &sb);
+    if (e == hipSuccess) e = sc.flag(st, &err);
     if (e != hipSuccess) return fail(BKD_ERR_NOMEM, std::string("plan scratch: ") + hipGetErrorString(e));
     uint32_t *blk = Carver::at<uint32_t>(sb, o_blk),
              *blkoff = Carver::at<uint32_t>(sb, o_blkoff), *hdr = Carver::at<uint32_t>(sb, o_hdr),
@@ -315,7 +372,7 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     const uint32_t* btab = tab + bkd::gf2::byte_table_offset(G);
     hipLaunchKernelGGL(bkd::plan_combine_kernel, dim3(nb * reps), dim3(1024), 0, st, base, offsets, lengths, seeds,
                        seed_all, size, n, pg, xtab, bkd::gf2::xpow(algo, 8ull * pg.ch), tab + 1024, btab, ds.xinv[algo],
-                       bkd::gf2::poly(algo), pslot, partials, out, ds.err, reps);
+                       bkd::gf2::poly(algo), pslot, partials, out, err, reps);
     e = hipGetLastError();
     if (e != hipSuccess) return fail(BKD_ERR_HIP, std::string("plan kernels: ") + hipGetErrorString(e));
     return BKD_OK;
@@ -328,8 +385,15 @@ int indexed_batch(DeviceState& ds, int algo, const uint8_t* base, uint64_t size,
     // plan descriptors hold 41-bit offsets (PlanDesc): larger buffers take the direct kernel
     const bool direct = mode == 1 || (mode == 0 && size <= kDirectMaxBytes) || size >= bkd::kPlanMaxSize;
     if (!direct) return launch_plan(ds, algo, base, size, offsets, lengths, n, seeds, seed_all, out, st);
+    uint32_t* err = nullptr;
+    {
+        StreamScratch& sc = scratch_for(ds, st);
+        std::lock_guard<std::recursive_mutex> lk(sc.mu);
+        const hipError_t e = sc.flag(st, &err);
+        if (e != hipSuccess) return fail(BKD_ERR_NOMEM, std::string("bounds flag: ") + hipGetErrorString(e));
+    }
     bkd::IndexedSrc src{n, offsets, lengths, seeds, seed_all, size, out};
-    return dispatch_lanes(ds, auto_lanes(n ? size / n : 0, n, ds.cus), algo, base, src, n, st);
+    return dispatch_lanes(ds, auto_lanes(n ? size / n : 0, n, ds.cus), algo, base, src, n, st, err);
 }
 
 bool valid_algo(int algo) { return algo == BKD_CRC32C || algo == BKD_CRC32; }
@@ -365,6 +429,25 @@ struct HostStage {
     uint32_t* d_res[2] = {};
     hipStream_t st[2] = {};
     hipEvent_t done[2] = {};
+    // framed-entry batches (bkd_digest_*_batch_host), allocated on first use: per-entry ids, LACs
+    // and length fields in (24 B per entry), frame headers and first_bad out
+    static constexpr size_t kAux = 64u << 20;
+    bool aux_ready = false;
+    uint8_t* h_aux[2] = {};
+    uint8_t* d_aux[2] = {};
+    uint8_t* h_frm[2] = {};
+    uint8_t* d_frm[2] = {};
+    int init_aux() {
+        if (aux_ready) return BKD_OK;
+        for (int s = 0; s < 2; ++s) {
+            BKD_HIP(hipHostMalloc((void**)&h_aux[s], kAux, hipHostMallocDefault));
+            BKD_HIP(hipMalloc((void**)&d_aux[s], kAux));
+            BKD_HIP(hipHostMalloc((void**)&h_frm[s], kAux, hipHostMallocDefault));
+            BKD_HIP(hipMalloc((void**)&d_frm[s], kAux));
+        }
+        aux_ready = true;
+        return BKD_OK;
+    }
     int init() {
         if (ready) return BKD_OK;
         for (int s = 0; s < 2; ++s) {
@@ -386,6 +469,105 @@ struct HostStage {
     }
 };
 HostStage g_stage[kMaxDevices];
+
+// Host threads for the copies into pinned staging (a pageable source, or a list of separate
+// entry buffers such as a ByteBufList): one core copies ~10-20 GB/s, below PCIe Gen5's ~55.
+class CopyPool {
+  public:
+    static CopyPool& get() {
+        static CopyPool pool;
+        return pool;
+    }
+    // Runs f(part) for part = 0..parts-1 (part 0 on the calling thread) and waits for all.
+    void run(int parts, const std::function<void(int)>& f) {
+        parts = std::max(1, std::min(parts, (int)workers_.size() + 1));
+        if (parts == 1) return f(0);
+        std::unique_lock<std::mutex> call(call_mu_);  // one parallel copy at a time
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            job_ = &f;
+            parts_ = parts;
+            pending_ = parts - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+    int threads() const { return (int)workers_.size() + 1; }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : workers_) t.join();
+    }
+
+  private:
+    CopyPool() {
+        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        const int n = (int)std::min(8u, std::max(1u, hw / 2)) - 1;
+        for (int w = 0; w < n; ++w) workers_.emplace_back([this, w] { loop(w + 1); });
+    }
+    void loop(int part) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(int)>* f = nullptr;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                if (part >= parts_) continue;
+                f = job_;
+            }
+            (*f)(part);
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--pending_ == 0) done_.notify_all();
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex mu_, call_mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)>* job_ = nullptr;
+    int parts_ = 0, pending_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+// memcpy of one range on the copy pool (parts of >= 4 MiB).
+void parallel_copy(uint8_t* dst, const uint8_t* src, size_t n) {
+    CopyPool& pool = CopyPool::get();
+    const int parts = (int)std::min<size_t>((size_t)pool.threads(), std::max<size_t>(1, n >> 22));
+    const size_t per = (n + parts - 1) / parts;
+    pool.run(parts, [&](int p) {
+        const size_t a = std::min(n, per * (size_t)p), b = std::min(n, a + per);
+        if (b > a) memcpy(dst + a, src + a, b - a);
+    });
+}
+
+// Packs entries src[i] (len[i] bytes) back to back into dst; off[i] = where entry i landed.
+// Split over the copy pool by bytes.
+void gather_entries(const void* const* src, const uint32_t* len, uint64_t cnt, uint8_t* dst, uint64_t* off) {
+    uint64_t at = 0;
+    for (uint64_t i = 0; i < cnt; ++i) {
+        off[i] = at;
+        at += len[i];
+    }
+    CopyPool& pool = CopyPool::get();
+    const int parts = (int)std::min<uint64_t>((uint64_t)pool.threads(), std::max<uint64_t>(1, at >> 22));
+    const uint64_t per = (at + parts - 1) / parts;
+    pool.run(parts, [&](int p) {
+        // entries whose first byte lies in [p*per, (p+1)*per)
+        const uint64_t lo = per * (uint64_t)p, hi = lo + per;
+        uint64_t i = (uint64_t)(std::lower_bound(off, off + cnt, lo) - off);
+        for (; i < cnt && off[i] < hi; ++i)
+            if (len[i]) memcpy(dst + off[i], src[i], len[i]);
+    });
+}
 
 int indexed_batch(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, const uint64_t* offsets,
                   const uint32_t* lengths, uint64_t n, const uint32_t* seeds, uint32_t seed_all, uint32_t* out,
@@ -474,7 +656,7 @@ int host_batch_pipelined(DeviceState& ds, HostStage& hs, int algo, const uint8_t
         if (h_seeds) memcpy(hs.h_seed[s], h_seeds + i0, cnt * 4);
         const uint8_t* src = h_base + b0;
         if (!pinned) {
-            memcpy(hs.h_pin[s], src, span);
+            parallel_copy(hs.h_pin[s], src, span);
             src = hs.h_pin[s];
         }
         hipStream_t st = hs.st[s];
@@ -504,20 +686,202 @@ int host_batch_pipelined(DeviceState& ds, HostStage& hs, int algo, const uint8_t
     return rc ? rc : (r0 ? r0 : r1);
 }
 
+// ---- DigestManager batch framing: the device sequences shared by the device- and host-resident
+// entry points -------------------------------------------------------------------------------
+
+// Package: header kernel (32 B BE header, header CRC as the payload's seed) -> payload CRCs through
+// the direct kernel -> digest kernel (BE digest after the header). Out-of-range payload entries
+// raise the stream's bounds flag.
+int package_framed(DeviceState& ds, hipStream_t st, int algo, int64_t ledger_id, const int64_t* d_entry_ids,
+                   const int64_t* d_lacs, const int64_t* d_length_fields, const void* d_payload,
+                   uint64_t payload_size, const uint64_t* d_offsets, const uint32_t* d_lengths, uint64_t n,
+                   void* d_frames, uint64_t frame_stride, uint32_t* d_digests) {
+    const uint32_t mac = algo == BKD_CRC32C ? 4u : 8u;
+    const int lanes = auto_lanes(payload_size / n, n, ds.cus);
+    const uint32_t* tab = ds.tables[algo][lane_index(lanes)];
+    uint32_t* err = nullptr;
+    {
+        StreamScratch& sc = scratch_for(ds, st);
+        std::lock_guard<std::recursive_mutex> lk(sc.mu);
+        const hipError_t e = sc.flag(st, &err);
+        if (e != hipSuccess) return fail(BKD_ERR_NOMEM, std::string("bounds flag: ") + hipGetErrorString(e));
+    }
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(bkd::package_header_kernel, dim3(blocks), dim3(256), 0, st, tab + 1024, ledger_id, d_entry_ids,
+                       d_lacs, d_length_fields, n, (uint8_t*)d_frames, frame_stride, d_digests);
+    BKD_HIP(hipGetLastError());
+    bkd::IndexedSrc src{n, d_offsets, d_lengths, d_digests, 0u, payload_size, d_digests};
+    int rc = dispatch_lanes(ds, lanes, algo, (const uint8_t*)d_payload, src, n, st, err);
+    if (rc) return rc;
+    hipLaunchKernelGGL(bkd::package_digest_kernel, dim3(blocks), dim3(256), 0, st, d_digests, n,
+                       (uint8_t*)d_frames, frame_stride, mac);
+    BKD_HIP(hipGetLastError());
+    return BKD_OK;
+}
+
+// Verify (bkd_digest_verify_batch and bkd_entrylog_verify): header CRCs -> payload CRCs seeded
+// with them through the indexed path (chunked plan for large ragged batches) -> compare.
+int verify_framed(DeviceState& ds, hipStream_t st, int algo, int64_t ledger_id, int64_t first_entry_id,
+                  int id_checks, const void* d_framed, uint64_t framed_size, const uint64_t* d_offsets,
+                  const uint32_t* d_lengths, uint64_t n, int32_t* d_status, uint64_t* d_first_bad) {
+    const uint32_t mac = algo == BKD_CRC32C ? 4u : 8u;
+    if (n == 0) {
+        BKD_HIP(hipMemsetAsync(d_first_bad, 0, sizeof(uint64_t), st));
+        return BKD_OK;
+    }
+    const uint32_t* x32tab = ds.tables[algo][lane_index(4)] + 1024;  // x^32 operator, 4 x 256
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    Carver cv;
+    const size_t o_seeds = cv.take(n * 4), o_plen = cv.take(n * 4), o_poff = cv.take(n * 8), o_exp = cv.take(n * 4),
+                 o_pre = cv.take(n * 4);
+    StreamScratch& sc = scratch_for(ds, st);
+    std::lock_guard<std::recursive_mutex> lk(sc.mu);  // held across the nested plan (slot 0)
+    uint8_t* sb = nullptr;
+    hipError_t e = sc.get(1, cv.used, st, &sb);
+    if (e != hipSuccess) return fail(BKD_ERR_NOMEM, std::string("verify scratch: ") + hipGetErrorString(e));
+    uint32_t* seeds = Carver::at<uint32_t>(sb, o_seeds);
+    uint32_t* plen = Carver::at<uint32_t>(sb, o_plen);
+    uint64_t* poff = Carver::at<uint64_t>(sb, o_poff);
+    uint32_t* expect = Carver::at<uint32_t>(sb, o_exp);
+    uint32_t* pre = Carver::at<uint32_t>(sb, o_pre);
+    hipLaunchKernelGGL(bkd::verify_header_kernel, dim3(blocks), dim3(256), 0, st, x32tab, (const uint8_t*)d_framed,
+                       framed_size, d_offsets, d_lengths, n, mac, ledger_id, first_entry_id, id_checks, seeds, poff,
+                       plen, expect, pre, d_first_bad);
+    e = hipGetLastError();
+    if (e != hipSuccess) return fail(BKD_ERR_HIP, hipGetErrorString(e));
+    // payload CRCs land in d_status, then verify_finish turns them into status codes
+    int rc = indexed_batch(ds, algo, (const uint8_t*)d_framed, framed_size, poff, plen, n, seeds, 0,
+                           reinterpret_cast<uint32_t*>(d_status), st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(bkd::verify_finish_kernel, dim3(blocks), dim3(256), 0, st, expect, pre, n, d_status,
+                       (unsigned long long*)d_first_bad);
+    e = hipGetLastError();
+    if (e != hipSuccess) return fail(BKD_ERR_HIP, hipGetErrorString(e));
+    return BKD_OK;
+}
+
+// ---- host-resident framed batches (BatchedReadOp's ByteBufList, PendingAddOp's payloads) ----
+// Entries are separate host buffers. Segments of <= kSeg bytes / kSegEntries entries are gathered
+// back to back into the slot's pinned buffer on the copy pool, copied H2D on the slot's stream,
+// run through the device sequence, and the per-entry results copied D2H; slot k % 2 alternates
+// so one segment's gather and H2D overlap the other's kernels and D2H.
+template <class Seg, class Drain>
+int host_segments(HostStage& hs, const uint32_t* h_lengths, uint64_t n, uint64_t max_entries, Seg&& seg,
+                  Drain&& drain_slot) {
+    uint64_t pend_i0[2] = {0, 0}, pend_cnt[2] = {0, 0};
+    bool busy[2] = {false, false};
+    auto drain = [&](int s) -> int {
+        if (!busy[s]) return BKD_OK;
+        BKD_HIP(hipEventSynchronize(hs.done[s]));
+        busy[s] = false;
+        return drain_slot(s, pend_i0[s], pend_cnt[s]);
+    };
+    int rc = BKD_OK;
+    uint64_t i0 = 0;
+    for (int k = 0; i0 < n && rc == BKD_OK; ++k) {
+        const int s = k & 1;
+        uint64_t i1 = i0, bytes = 0;
+        while (i1 < n && i1 - i0 < max_entries && (i1 == i0 || bytes + h_lengths[i1] <= HostStage::kSeg))
+            bytes += h_lengths[i1++];
+        if (bytes > HostStage::kSeg) return fail(BKD_ERR_INVALID_ARG, "a host entry is larger than 64 MiB");
+        if ((rc = drain(s))) break;
+        if ((rc = seg(s, i0, i1 - i0, bytes))) break;
+        BKD_HIP(hipEventRecord(hs.done[s], hs.st[s]));
+        busy[s] = true;
+        pend_i0[s] = i0;
+        pend_cnt[s] = i1 - i0;
+        i0 = i1;
+    }
+    const int r0 = drain(0), r1 = drain(1);
+    return rc ? rc : (r0 ? r0 : r1);
+}
+
+// ---- per-call resume (IntHash.resume) -------------------------------------------------------
+// Host buffers up to this many bytes take the CPU route (host_crc.cpp); larger ones the GPU
+// through pinned staging. Default 4 MiB: where a pageable source breaks even (one core ~210 us vs
+// ~230 us by gather + PCIe + launch, profiles/r02_call_latency.log).
+std::atomic<uint64_t> g_cpu_route_max{(uint64_t)4 << 20};
+
+int cpu_resume(int algo, uint32_t current, const void* p, uint64_t len, uint32_t* out) {
+    *out = ~bkd::host::crc_raw(algo, ~current, (const uint8_t*)p, (size_t)len);
+    return BKD_OK;
+}
+
+// Device scratch of one synchronous per-call resume, pooled per device (no per-thread state
+// that outlives its thread, no allocation on the hot path after the first calls).
+struct CallScratch {
+    uint32_t* d_out = nullptr;
+    uint64_t* d_off = nullptr;
+    uint32_t* d_len = nullptr;
+    uint32_t* h_out = nullptr;  // pinned: [0] result, [1] length for the plan path
+};
+struct CallPool {
+    std::mutex mu;
+    std::vector<CallScratch*> free;
+};
+CallPool g_call_pool[kMaxDevices];
+
+int call_acquire(int dev, hipStream_t st, CallScratch** out) {
+    CallPool& p = g_call_pool[dev];
+    {
+        std::lock_guard<std::mutex> lk(p.mu);
+        if (!p.free.empty()) {
+            *out = p.free.back();
+            p.free.pop_back();
+            return BKD_OK;
+        }
+    }
+    std::unique_ptr<CallScratch> c(new CallScratch());
+    BKD_HIP(hipMalloc((void**)&c->d_out, 4));
+    BKD_HIP(hipMalloc((void**)&c->d_off, 8));
+    BKD_HIP(hipMalloc((void**)&c->d_len, 4));
+    BKD_HIP(hipHostMalloc((void**)&c->h_out, 8, hipHostMallocDefault));
+    BKD_HIP(hipMemsetAsync(c->d_off, 0, 8, st));
+    *out = c.release();
+    return BKD_OK;
+}
+
+void call_release(int dev, CallScratch* c) {
+    std::lock_guard<std::mutex> lk(g_call_pool[dev].mu);
+    g_call_pool[dev].free.push_back(c);
+}
+
+int resume_device(int algo, uint32_t current, const void* ptr, uint64_t len, hipStream_t st, uint32_t* out) {
+    DeviceScope scope;
+    DeviceState* ds = nullptr;
+    int rc = enter(st, scope, &ds);
+    if (rc) return rc;
+    const int dev = (int)(ds - g_dev);
+    CallScratch* c = nullptr;
+    if ((rc = call_acquire(dev, st, &c))) return rc;
+    const uint32_t l32 = (uint32_t)len;
+    if (len < (1u << 20)) {  // one group: the entry as a uniform batch of one
+        bkd::UniformSrc src{1, len, l32, nullptr, current, c->d_out};
+        rc = dispatch_lanes(*ds, auto_lanes(len, 1, ds->cus), algo, (const uint8_t*)ptr, src, 1, st);
+    } else {  // large: the chunked plan spreads it over the chip
+        c->h_out[1] = l32;
+        const hipError_t e = hipMemcpyAsync(c->d_len, c->h_out + 1, 4, hipMemcpyHostToDevice, st);
+        rc = e == hipSuccess ? launch_plan(*ds, algo, (const uint8_t*)ptr, len, c->d_off, c->d_len, 1, nullptr,
+                                           current, c->d_out, st)
+                             : fail(BKD_ERR_HIP, hipGetErrorString(e));
+    }
+    if (!rc) {
+        hipError_t e = hipMemcpyAsync(c->h_out, c->d_out, 4, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) rc = fail(BKD_ERR_HIP, std::string("resume: ") + hipGetErrorString(e));
+        else *out = c->h_out[0];
+    }
+    call_release(dev, c);
+    return rc;
+}
+
 }  // namespace
 
 extern "C" {
 
 int bkd_abi_version(void) { return BKD_ABI_VERSION; }
 
-int bkd_device_count(void) {
-    int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess) {
-        (void)hipGetLastError();
-        return 0;
-    }
-    return count;
-}
+int bkd_device_count(void) { return std::max(0, visible_devices()); }
 
 int bkd_init(int device) {
     int count = bkd_device_count();
@@ -572,8 +936,10 @@ int bkd_crc_batch_uniform(int algo, const void* d_base, uint64_t stride, uint32_
     if (!valid_algo(algo)) return fail(BKD_ERR_INVALID_ARG, "unknown algorithm");
     if (n && (!d_base || !d_out)) return fail(BKD_ERR_INVALID_ARG, "null buffer");
     if (n > 1 && stride < entry_len) return fail(BKD_ERR_INVALID_ARG, "stride < entry_len");
+    const hipStream_t st = (hipStream_t)stream;
+    DeviceScope scope;
     DeviceState* ds = nullptr;
-    int rc = ensure_current(&ds);
+    int rc = enter(st, scope, &ds);
     if (rc) return rc;
     bkd::UniformSrc src{n, stride, entry_len, d_seeds, seed_all, d_out};
     // entries of 16..48 B: one lane per entry, both loads of an entry in flight with the next
@@ -581,7 +947,7 @@ int bkd_crc_batch_uniform(int algo, const void* d_base, uint64_t stride, uint32_
     int lanes = auto_lanes(entry_len, n, ds->cus);
     if (g_forced_lanes.load() == 0 && entry_len >= 16u && entry_len <= 48u && n >= (uint64_t)ds->cus * bkd::kBlock)
         lanes = 1;
-    return dispatch_lanes(*ds, lanes, algo, (const uint8_t*)d_base, src, n, (hipStream_t)stream);
+    return dispatch_lanes(*ds, lanes, algo, (const uint8_t*)d_base, src, n, st);
 }
 
 int bkd_crc_batch(int algo, const void* d_base, uint64_t base_size, const uint64_t* d_offsets,
@@ -590,24 +956,32 @@ int bkd_crc_batch(int algo, const void* d_base, uint64_t base_size, const uint64
     if (!valid_algo(algo)) return fail(BKD_ERR_INVALID_ARG, "unknown algorithm");
     if (n && (!d_offsets || !d_lengths || !d_out)) return fail(BKD_ERR_INVALID_ARG, "null index/out");
     if (n && !d_base && base_size) return fail(BKD_ERR_INVALID_ARG, "null base");
+    const hipStream_t st = (hipStream_t)stream;
+    DeviceScope scope;
     DeviceState* ds = nullptr;
-    int rc = ensure_current(&ds);
+    int rc = enter(st, scope, &ds);
     if (rc) return rc;
     return indexed_batch(*ds, algo, (const uint8_t*)d_base, base_size, d_offsets, d_lengths, n, d_seeds, seed_all,
-                         d_out, (hipStream_t)stream);
+                         d_out, st);
 }
 
 int bkd_stream_sync(void* stream) {
+    const hipStream_t st = (hipStream_t)stream;
+    DeviceScope scope;
     DeviceState* ds = nullptr;
-    int rc = ensure_current(&ds);
+    int rc = enter(st, scope, &ds);
     if (rc) return rc;
-    BKD_HIP(hipStreamSynchronize((hipStream_t)stream));
-    uint32_t flag = 0;
-    BKD_HIP(hipMemcpy(&flag, ds->err, sizeof(flag), hipMemcpyDeviceToHost));
-    if (flag) {
-        BKD_HIP(hipMemset(ds->err, 0, sizeof(uint32_t)));
-        return fail(BKD_ERR_BOUNDS, "an indexed entry exceeded its base buffer (entries skipped, out = 0)");
+    StreamScratch& sc = scratch_for(*ds, st);
+    std::lock_guard<std::recursive_mutex> lk(sc.mu);
+    if (!sc.err) {  // nothing indexed was ever enqueued on this stream
+        BKD_HIP(hipStreamSynchronize(st));
+        return BKD_OK;
     }
+    // read and clear this stream's flag in stream order, after the work it guards
+    BKD_HIP(hipMemcpyAsync(sc.h_err, sc.err, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    BKD_HIP(hipMemsetAsync(sc.err, 0, sizeof(uint32_t), st));
+    BKD_HIP(hipStreamSynchronize(st));
+    if (*sc.h_err) return fail(BKD_ERR_BOUNDS, "an indexed entry exceeded its base buffer (entries skipped, out = 0)");
     return BKD_OK;
 }
 
@@ -623,12 +997,11 @@ int bkd_crc_batch_host(int algo, const void* h_base, uint64_t base_size, const u
             return fail(BKD_ERR_BOUNDS, "entry " + std::to_string(i) + " exceeds base buffer");
         if (i && h_offsets[i] < h_offsets[i - 1]) sorted = false;
     }
+    DeviceScope scope;
     DeviceState* ds = nullptr;
-    int rc = ensure_current(&ds);
+    int rc = enter(nullptr, scope, &ds);
     if (rc) return rc;
-    int dev = 0;
-    BKD_HIP(hipGetDevice(&dev));
-    HostStage& hs = g_stage[dev];
+    HostStage& hs = g_stage[ds - g_dev];
     std::lock_guard<std::mutex> lk(hs.mu);
     rc = hs.init();
     if (rc) return rc;
@@ -638,62 +1011,80 @@ int bkd_crc_batch_host(int algo, const void* h_base, uint64_t base_size, const u
                                 h_out);
 }
 
-int bkd_resume(int algo, uint32_t current, const void* ptr, uint64_t len, uint32_t* out) {
+int bkd_cpu_resume(int algo, uint32_t current, const void* h_ptr, uint64_t len, uint32_t* out) {
+    if (!valid_algo(algo)) return fail(BKD_ERR_INVALID_ARG, "unknown algorithm");
+    if (!out) return fail(BKD_ERR_INVALID_ARG, "null out");
+    if (len && !h_ptr) return fail(BKD_ERR_INVALID_ARG, "null buffer");
+    return cpu_resume(algo, current, h_ptr, len, out);
+}
+
+int bkd_resume_host(int algo, uint32_t current, const void* h_ptr, uint64_t len, uint32_t* out) {
+    if (!valid_algo(algo)) return fail(BKD_ERR_INVALID_ARG, "unknown algorithm");
+    if (!out) return fail(BKD_ERR_INVALID_ARG, "null out");
+    if (len == 0) {  // crc32c_sse42.cpp:211-213: resume of nothing returns the seed
+        *out = current;
+        return BKD_OK;
+    }
+    if (!h_ptr) return fail(BKD_ERR_INVALID_ARG, "null buffer");
+    if (len <= g_cpu_route_max.load(std::memory_order_relaxed) || visible_devices() <= 0)
+        return cpu_resume(algo, current, h_ptr, len, out);
+    if (len > 0xFFFFFFFFull) return fail(BKD_ERR_INVALID_ARG, "len > 4 GiB - 1");
+    const uint64_t off = 0;
+    const uint32_t l32 = (uint32_t)len;
+    return bkd_crc_batch_host(algo, h_ptr, len, &off, &l32, 1, nullptr, current, out);
+}
+
+int bkd_resume_device(int algo, uint32_t current, const void* d_ptr, uint64_t len, void* stream, uint32_t* out) {
     if (!valid_algo(algo)) return fail(BKD_ERR_INVALID_ARG, "unknown algorithm");
     if (!out) return fail(BKD_ERR_INVALID_ARG, "null out");
     if (len > 0xFFFFFFFFull) return fail(BKD_ERR_INVALID_ARG, "len > 4 GiB - 1");
-    if (len == 0) {  // crc32c_sse42.cpp:211-213: resume of nothing returns the seed
-        DeviceState* ds = nullptr;
-        int rc = ensure_current(&ds);
-        if (rc) return rc;
+    if (len == 0) {
+        *out = current;
+        return BKD_OK;
+    }
+    if (!d_ptr) return fail(BKD_ERR_INVALID_ARG, "null buffer");
+    return resume_device(algo, current, d_ptr, len, (hipStream_t)stream, out);
+}
+
+int bkd_resume(int algo, uint32_t current, const void* ptr, uint64_t len, uint32_t* out) {
+    if (!valid_algo(algo)) return fail(BKD_ERR_INVALID_ARG, "unknown algorithm");
+    if (!out) return fail(BKD_ERR_INVALID_ARG, "null out");
+    if (len == 0) {
         *out = current;
         return BKD_OK;
     }
     if (!ptr) return fail(BKD_ERR_INVALID_ARG, "null buffer");
-    const uint64_t off = 0;
-    const uint32_t l32 = (uint32_t)len;
-    if (is_device_pointer(ptr)) {
-        DeviceState* ds = nullptr;
-        int rc = ensure_current(&ds);
-        if (rc) return rc;
-        int dev = 0;
-        BKD_HIP(hipGetDevice(&dev));
-        // per-thread, per-device scratch: no allocation (hipFree synchronises the whole device)
-        // and no shared state on this latency path
-        struct CallScratch {
-            hipStream_t st = nullptr;
-            uint32_t* d_out = nullptr;
-            uint64_t* d_off = nullptr;
-            uint32_t* d_len = nullptr;
-            uint32_t* h_out = nullptr;  // pinned: [0] result, [1] length for the plan path
-        };
-        thread_local CallScratch cs[kMaxDevices];
-        CallScratch& c = cs[dev];
-        if (!c.st) {
-            BKD_HIP(hipStreamCreateWithFlags(&c.st, hipStreamNonBlocking));
-            BKD_HIP(hipMalloc((void**)&c.d_out, 4));
-            BKD_HIP(hipMalloc((void**)&c.d_off, 8));
-            BKD_HIP(hipMalloc((void**)&c.d_len, 4));
-            BKD_HIP(hipHostMalloc((void**)&c.h_out, 8, hipHostMallocDefault));
-            BKD_HIP(hipMemsetAsync(c.d_off, 0, 8, c.st));
-        }
-        if (len < (1u << 20)) {  // one group: the entry as a uniform batch of one
-            bkd::UniformSrc src{1, len, l32, nullptr, current, c.d_out};
-            rc = dispatch_lanes(*ds, auto_lanes(len, 1, ds->cus), algo, (const uint8_t*)ptr, src, 1, c.st);
-        } else {  // large: the chunked plan spreads it over the chip
-            c.h_out[1] = l32;
-            BKD_HIP(hipMemcpyAsync(c.d_len, c.h_out + 1, 4, hipMemcpyHostToDevice, c.st));
-            rc = launch_plan(*ds, algo, (const uint8_t*)ptr, len, c.d_off, c.d_len, 1, nullptr, current, c.d_out,
-                             c.st);
-        }
-        if (rc) return rc;
-        BKD_HIP(hipMemcpyAsync(c.h_out, c.d_out, 4, hipMemcpyDeviceToHost, c.st));
-        BKD_HIP(hipStreamSynchronize(c.st));
-        *out = *c.h_out;
-        return BKD_OK;
-    }
-    return bkd_crc_batch_host(algo, ptr, len, &off, &l32, 1, nullptr, current, out);
+    // a device buffer runs on the null stream, which orders the call after the work queued on
+    // the blocking streams (PyTorch's default stream among them) that may still be writing it
+    if (visible_devices() > 0 && is_device_pointer(ptr))
+        return bkd_resume_device(algo, current, ptr, len, nullptr, out);
+    return bkd_resume_host(algo, current, ptr, len, out);
 }
+
+int bkd_circe_supported(void) { return 1; }
+
+int64_t bkd_circe_alloc_config(const int32_t* chunk_words, int32_t len) {
+    constexpr int32_t kMinWords = 4;  // chunk_config::min_words (crc32c_sse42.hpp:22)
+    if (!chunk_words || len < 1 || chunk_words[0] < kMinWords) return 0;
+    for (int32_t i = 1; i < len; ++i)
+        if (chunk_words[i] < kMinWords || chunk_words[i] >= chunk_words[i - 1]) return 0;  // strictly decreasing
+    int32_t* cfg = new (std::nothrow) int32_t[(size_t)len + 1];
+    if (!cfg) return 0;
+    cfg[0] = len;
+    memcpy(cfg + 1, chunk_words, (size_t)len * sizeof(int32_t));
+    return (int64_t)(intptr_t)cfg;
+}
+
+void bkd_circe_free_config(int64_t config) { delete[] (int32_t*)(intptr_t)config; }
+
+int bkd_set_cpu_route_max(uint64_t bytes) {
+    g_cpu_route_max.store(bytes);
+    return BKD_OK;
+}
+
+uint64_t bkd_get_cpu_route_max(void) { return g_cpu_route_max.load(); }
+
+const char* bkd_cpu_impl(void) { return bkd::host::impl_name(); }
 
 int bkd_digest_package_batch(int algo, int64_t ledger_id, const int64_t* d_entry_ids, const int64_t* d_lacs,
                              const int64_t* d_length_fields, const void* d_payload, uint64_t payload_size,
@@ -705,92 +1096,134 @@ int bkd_digest_package_batch(int algo, int64_t ledger_id, const int64_t* d_entry
     if (!d_entry_ids || !d_lacs || !d_length_fields || !d_offsets || !d_lengths || !d_frames || !d_digests)
         return fail(BKD_ERR_INVALID_ARG, "null buffer");
     if (frame_stride < 32u + mac) return fail(BKD_ERR_INVALID_ARG, "frame_stride < 32 + digest length");
+    const hipStream_t st = (hipStream_t)stream;
+    DeviceScope scope;
     DeviceState* ds = nullptr;
-    int rc = ensure_current(&ds);
+    int rc = enter(st, scope, &ds);
     if (rc) return rc;
-    hipStream_t st = (hipStream_t)stream;
-    const int lanes = auto_lanes(payload_size / n, n, ds->cus);
-    const uint32_t* tab = ds->tables[algo][lane_index(lanes)];
-    const unsigned blocks = (unsigned)((n + 255) / 256);
-    hipLaunchKernelGGL(bkd::package_header_kernel, dim3(blocks), dim3(256), 0, st, tab + 1024, ledger_id, d_entry_ids,
-                       d_lacs, d_length_fields, n, (uint8_t*)d_frames, frame_stride, d_digests);
-    BKD_HIP(hipGetLastError());
-    bkd::IndexedSrc src{n, d_offsets, d_lengths, d_digests, 0u, payload_size, d_digests};
-    rc = dispatch_lanes(*ds, lanes, algo, (const uint8_t*)d_payload, src, n, st);
-    if (rc) return rc;
-    hipLaunchKernelGGL(bkd::package_digest_kernel, dim3(blocks), dim3(256), 0, st, d_digests, n,
-                       (uint8_t*)d_frames, frame_stride, mac);
-    BKD_HIP(hipGetLastError());
-    return BKD_OK;
+    return package_framed(*ds, st, algo, ledger_id, d_entry_ids, d_lacs, d_length_fields, d_payload, payload_size,
+                          d_offsets, d_lengths, n, d_frames, frame_stride, d_digests);
 }
-
-namespace {
-// Shared by bkd_digest_verify_batch and bkd_entrylog_verify: header CRCs -> payload CRCs seeded
-// with them through the indexed path (chunked plan for large ragged batches) -> compare.
-int verify_framed(int algo, int64_t ledger_id, int64_t first_entry_id, int id_checks, const void* d_framed,
-                  uint64_t framed_size, const uint64_t* d_offsets, const uint32_t* d_lengths, uint64_t n,
-                  int32_t* d_status, uint64_t* d_first_bad, void* stream) {
-    if (!valid_algo(algo)) return fail(BKD_ERR_INVALID_ARG, "unknown algorithm");
-    const uint32_t mac = algo == BKD_CRC32C ? 4u : 8u;
-    if (!d_first_bad) return fail(BKD_ERR_INVALID_ARG, "null first_bad");
-    if (n && (!d_offsets || !d_lengths || !d_status)) return fail(BKD_ERR_INVALID_ARG, "null buffer");
-    if (n && !d_framed) return fail(BKD_ERR_INVALID_ARG, "null framed buffer");
-    DeviceState* ds = nullptr;
-    int rc = ensure_current(&ds);
-    if (rc) return rc;
-    hipStream_t st = (hipStream_t)stream;
-    if (n == 0) {
-        BKD_HIP(hipMemsetAsync(d_first_bad, 0, sizeof(uint64_t), st));
-        return BKD_OK;
-    }
-    const uint32_t* x32tab = ds->tables[algo][lane_index(4)] + 1024;  // x^32 operator, 4 x 256
-    const unsigned blocks = (unsigned)((n + 255) / 256);
-    Carver cv;
-    const size_t o_seeds = cv.take(n * 4), o_plen = cv.take(n * 4), o_poff = cv.take(n * 8), o_exp = cv.take(n * 4),
-                 o_pre = cv.take(n * 4);
-    StreamScratch& sc = scratch_for(*ds, st);
-    std::lock_guard<std::recursive_mutex> lk(sc.mu);  // held across the nested plan (slot 0)
-    uint8_t* sb = nullptr;
-    hipError_t e = sc.get(1, cv.used, st, &sb);
-    uint32_t* seeds = Carver::at<uint32_t>(sb, o_seeds);
-    uint32_t* plen = Carver::at<uint32_t>(sb, o_plen);
-    uint64_t* poff = Carver::at<uint64_t>(sb, o_poff);
-    uint32_t* expect = Carver::at<uint32_t>(sb, o_exp);
-    uint32_t* pre = Carver::at<uint32_t>(sb, o_pre);
-    if (e != hipSuccess) {
-        rc = fail(BKD_ERR_NOMEM, std::string("verify scratch: ") + hipGetErrorString(e));
-    } else {
-        hipLaunchKernelGGL(bkd::verify_header_kernel, dim3(blocks), dim3(256), 0, st, x32tab,
-                           (const uint8_t*)d_framed, framed_size, d_offsets, d_lengths, n, mac, ledger_id,
-                           first_entry_id, id_checks, seeds, poff, plen, expect, pre, d_first_bad);
-        e = hipGetLastError();
-        if (e != hipSuccess) rc = fail(BKD_ERR_HIP, hipGetErrorString(e));
-        if (!rc)  // payload CRCs land in d_status, then verify_finish turns them into status codes
-            rc = indexed_batch(*ds, algo, (const uint8_t*)d_framed, framed_size, poff, plen, n, seeds, 0,
-                               reinterpret_cast<uint32_t*>(d_status), st);
-        if (!rc) {
-            hipLaunchKernelGGL(bkd::verify_finish_kernel, dim3(blocks), dim3(256), 0, st, expect, pre, n, d_status,
-                               (unsigned long long*)d_first_bad);
-            e = hipGetLastError();
-            if (e != hipSuccess) rc = fail(BKD_ERR_HIP, hipGetErrorString(e));
-        }
-    }
-    return rc;
-}
-}  // namespace
 
 int bkd_digest_verify_batch(int algo, int64_t ledger_id, int64_t first_entry_id, int skip_entry_check,
                             const void* d_framed, uint64_t framed_size, const uint64_t* d_offsets,
                             const uint32_t* d_lengths, uint64_t n, int32_t* d_status, uint64_t* d_first_bad,
                             void* stream) {
-    return verify_framed(algo, ledger_id, first_entry_id, skip_entry_check ? 1 : 0, d_framed, framed_size,
-                         d_offsets, d_lengths, n, d_status, d_first_bad, stream);
+    if (!valid_algo(algo)) return fail(BKD_ERR_INVALID_ARG, "unknown algorithm");
+    if (!d_first_bad) return fail(BKD_ERR_INVALID_ARG, "null first_bad");
+    if (n && (!d_offsets || !d_lengths || !d_status)) return fail(BKD_ERR_INVALID_ARG, "null buffer");
+    if (n && !d_framed) return fail(BKD_ERR_INVALID_ARG, "null framed buffer");
+    const hipStream_t st = (hipStream_t)stream;
+    DeviceScope scope;
+    DeviceState* ds = nullptr;
+    int rc = enter(st, scope, &ds);
+    if (rc) return rc;
+    return verify_framed(*ds, st, algo, ledger_id, first_entry_id, skip_entry_check ? 1 : 0, d_framed, framed_size,
+                         d_offsets, d_lengths, n, d_status, d_first_bad);
+}
+
+int bkd_digest_verify_batch_host(int algo, int64_t ledger_id, int64_t first_entry_id, int skip_entry_check,
+                                 const void* const* h_frames, const uint32_t* h_lengths, uint64_t n,
+                                 int32_t* h_status, uint64_t* h_first_bad) {
+    if (!valid_algo(algo)) return fail(BKD_ERR_INVALID_ARG, "unknown algorithm");
+    if (!h_first_bad) return fail(BKD_ERR_INVALID_ARG, "null first_bad");
+    *h_first_bad = n;
+    if (n == 0) return BKD_OK;
+    if (!h_frames || !h_lengths || !h_status) return fail(BKD_ERR_INVALID_ARG, "null buffer");
+    for (uint64_t i = 0; i < n; ++i)
+        if (h_lengths[i] && !h_frames[i]) return fail(BKD_ERR_INVALID_ARG, "null frame " + std::to_string(i));
+    DeviceScope scope;
+    DeviceState* ds = nullptr;
+    int rc = enter(nullptr, scope, &ds);
+    if (rc) return rc;
+    HostStage& hs = g_stage[ds - g_dev];
+    std::lock_guard<std::mutex> lk(hs.mu);
+    if ((rc = hs.init()) || (rc = hs.init_aux())) return rc;
+    const int id_checks = skip_entry_check ? 1 : 0;
+    auto seg = [&](int s, uint64_t i0, uint64_t cnt, uint64_t bytes) -> int {
+        gather_entries(h_frames + i0, h_lengths + i0, cnt, hs.h_pin[s], hs.h_off[s]);
+        const hipStream_t st = hs.st[s];
+        BKD_HIP(hipMemcpyAsync(hs.d_buf[s], hs.h_pin[s], bytes, hipMemcpyHostToDevice, st));
+        BKD_HIP(hipMemcpyAsync(hs.d_off[s], hs.h_off[s], cnt * 8, hipMemcpyHostToDevice, st));
+        BKD_HIP(hipMemcpyAsync(hs.d_len[s], h_lengths + i0, cnt * 4, hipMemcpyHostToDevice, st));
+        uint64_t* d_fb = reinterpret_cast<uint64_t*>(hs.d_frm[s]);
+        int r = verify_framed(*ds, st, algo, ledger_id, first_entry_id + (int64_t)i0, id_checks, hs.d_buf[s], bytes,
+                              hs.d_off[s], hs.d_len[s], cnt, reinterpret_cast<int32_t*>(hs.d_res[s]), d_fb);
+        if (r) return r;
+        BKD_HIP(hipMemcpyAsync(hs.h_res[s], hs.d_res[s], cnt * 4, hipMemcpyDeviceToHost, st));
+        BKD_HIP(hipMemcpyAsync(hs.h_frm[s], d_fb, 8, hipMemcpyDeviceToHost, st));
+        return BKD_OK;
+    };
+    auto drain = [&](int s, uint64_t i0, uint64_t cnt) -> int {
+        memcpy(h_status + i0, hs.h_res[s], cnt * 4);
+        const uint64_t fb = *reinterpret_cast<const uint64_t*>(hs.h_frm[s]);
+        if (fb < cnt && i0 + fb < *h_first_bad) *h_first_bad = i0 + fb;
+        return BKD_OK;
+    };
+    return host_segments(hs, h_lengths, n, HostStage::kSegEntries, seg, drain);
+}
+
+int bkd_digest_package_batch_host(int algo, int64_t ledger_id, const int64_t* h_entry_ids, const int64_t* h_lacs,
+                                  const int64_t* h_length_fields, const void* const* h_payloads,
+                                  const uint32_t* h_lengths, uint64_t n, void* h_frames, uint64_t frame_stride,
+                                  uint32_t* h_digests) {
+    if (!valid_algo(algo)) return fail(BKD_ERR_INVALID_ARG, "unknown algorithm");
+    const uint32_t mac = algo == BKD_CRC32C ? 4u : 8u;
+    if (n == 0) return BKD_OK;
+    if (!h_entry_ids || !h_lacs || !h_length_fields || !h_payloads || !h_lengths || !h_frames || !h_digests)
+        return fail(BKD_ERR_INVALID_ARG, "null buffer");
+    if (frame_stride < 32u + mac || frame_stride > 4096u)
+        return fail(BKD_ERR_INVALID_ARG, "frame_stride must be in [32 + digest length, 4096]");
+    for (uint64_t i = 0; i < n; ++i)
+        if (h_lengths[i] && !h_payloads[i]) return fail(BKD_ERR_INVALID_ARG, "null payload " + std::to_string(i));
+    DeviceScope scope;
+    DeviceState* ds = nullptr;
+    int rc = enter(nullptr, scope, &ds);
+    if (rc) return rc;
+    HostStage& hs = g_stage[ds - g_dev];
+    std::lock_guard<std::mutex> lk(hs.mu);
+    if ((rc = hs.init()) || (rc = hs.init_aux())) return rc;
+    const uint64_t max_entries = std::min<uint64_t>(HostStage::kSegEntries, HostStage::kAux / frame_stride);
+    auto seg = [&](int s, uint64_t i0, uint64_t cnt, uint64_t bytes) -> int {
+        gather_entries(h_payloads + i0, h_lengths + i0, cnt, hs.h_pin[s], hs.h_off[s]);
+        int64_t* aux = reinterpret_cast<int64_t*>(hs.h_aux[s]);
+        memcpy(aux, h_entry_ids + i0, cnt * 8);
+        memcpy(aux + cnt, h_lacs + i0, cnt * 8);
+        memcpy(aux + 2 * cnt, h_length_fields + i0, cnt * 8);
+        const hipStream_t st = hs.st[s];
+        BKD_HIP(hipMemcpyAsync(hs.d_buf[s], hs.h_pin[s], bytes, hipMemcpyHostToDevice, st));
+        BKD_HIP(hipMemcpyAsync(hs.d_off[s], hs.h_off[s], cnt * 8, hipMemcpyHostToDevice, st));
+        BKD_HIP(hipMemcpyAsync(hs.d_len[s], h_lengths + i0, cnt * 4, hipMemcpyHostToDevice, st));
+        BKD_HIP(hipMemcpyAsync(hs.d_aux[s], aux, cnt * 24, hipMemcpyHostToDevice, st));
+        const int64_t* d_aux = reinterpret_cast<const int64_t*>(hs.d_aux[s]);
+        int r = package_framed(*ds, st, algo, ledger_id, d_aux, d_aux + cnt, d_aux + 2 * cnt, hs.d_buf[s], bytes,
+                               hs.d_off[s], hs.d_len[s], cnt, hs.d_frm[s], frame_stride, hs.d_res[s]);
+        if (r) return r;
+        BKD_HIP(hipMemcpyAsync(hs.h_frm[s], hs.d_frm[s], cnt * frame_stride, hipMemcpyDeviceToHost, st));
+        BKD_HIP(hipMemcpyAsync(hs.h_res[s], hs.d_res[s], cnt * 4, hipMemcpyDeviceToHost, st));
+        return BKD_OK;
+    };
+    auto drain = [&](int s, uint64_t i0, uint64_t cnt) -> int {
+        memcpy((uint8_t*)h_frames + i0 * frame_stride, hs.h_frm[s], cnt * frame_stride);
+        memcpy(h_digests + i0, hs.h_res[s], cnt * 4);
+        return BKD_OK;
+    };
+    return host_segments(hs, h_lengths, n, max_entries, seg, drain);
 }
 
 int bkd_entrylog_verify(int algo, const void* d_log, uint64_t log_size, const uint64_t* d_offsets,
                         const uint32_t* d_lengths, uint64_t n, int32_t* d_status, uint64_t* d_first_bad,
                         void* stream) {
-    return verify_framed(algo, 0, 0, 2, d_log, log_size, d_offsets, d_lengths, n, d_status, d_first_bad, stream);
+    if (!valid_algo(algo)) return fail(BKD_ERR_INVALID_ARG, "unknown algorithm");
+    if (!d_first_bad) return fail(BKD_ERR_INVALID_ARG, "null first_bad");
+    if (n && (!d_offsets || !d_lengths || !d_status)) return fail(BKD_ERR_INVALID_ARG, "null buffer");
+    if (n && !d_log) return fail(BKD_ERR_INVALID_ARG, "null log buffer");
+    const hipStream_t st = (hipStream_t)stream;
+    DeviceScope scope;
+    DeviceState* ds = nullptr;
+    int rc = enter(st, scope, &ds);
+    if (rc) return rc;
+    return verify_framed(*ds, st, algo, 0, 0, 2, d_log, log_size, d_offsets, d_lengths, n, d_status, d_first_bad);
 }
 
 int bkd_crc_batch_segments(int algo, const void* d_base, uint64_t base_size, const uint64_t* d_seg_offsets,
@@ -801,10 +1234,11 @@ int bkd_crc_batch_segments(int algo, const void* d_base, uint64_t base_size, con
     if (!d_seg_first || !d_out || (nseg && (!d_seg_offsets || !d_seg_lengths)))
         return fail(BKD_ERR_INVALID_ARG, "null index/out");
     if (nseg && !d_base && base_size) return fail(BKD_ERR_INVALID_ARG, "null base");
+    const hipStream_t st = (hipStream_t)stream;
+    DeviceScope scope;
     DeviceState* ds = nullptr;
-    int rc = ensure_current(&ds);
+    int rc = enter(st, scope, &ds);
     if (rc) return rc;
-    hipStream_t st = (hipStream_t)stream;
     StreamScratch& sc = scratch_for(*ds, st);
     std::lock_guard<std::recursive_mutex> lk(sc.mu);  // held across the nested plan (slot 0)
     uint8_t* seg = nullptr;
@@ -821,7 +1255,7 @@ int bkd_crc_batch_segments(int algo, const void* d_base, uint64_t base_size, con
     for (int b = 0; b < 32; ++b) pw.p[b] = bkd::gf2::xpow(algo, 8ull << b);
     const unsigned blocks = (unsigned)((n + 255) / 256);
     hipLaunchKernelGGL(bkd::segments_combine_kernel, dim3(blocks), dim3(256), 0, st, d_seg_lengths, segcrc,
-                       d_seg_first, n, d_seeds, seed_all, pw, bkd::gf2::poly(algo), d_out);
+                       d_seg_first, n, nseg, d_seeds, seed_all, pw, bkd::gf2::poly(algo), d_out);
     BKD_HIP(hipGetLastError());
     return BKD_OK;
 }
@@ -876,12 +1310,14 @@ int bkd_entrylog_index(const void* h_log, uint64_t log_size, uint64_t start, uin
 int bkd_fill_splitmix64(void* d_dst, uint64_t nbytes, uint64_t seed, uint64_t first_word, void* stream) {
     if (nbytes == 0) return BKD_OK;
     if (!d_dst) return fail(BKD_ERR_INVALID_ARG, "null buffer");
+    const hipStream_t st = (hipStream_t)stream;
+    DeviceScope scope;
     DeviceState* ds = nullptr;
-    int rc = ensure_current(&ds);
+    int rc = enter(st, scope, &ds);
     if (rc) return rc;
     const uint64_t nw = std::max<uint64_t>(1, nbytes / 8);
     const unsigned blocks = (unsigned)std::min<uint64_t>((nw + 255) / 256, (uint64_t)ds->cus * 16);
-    hipLaunchKernelGGL(bkd::fill_splitmix64_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(bkd::fill_splitmix64_kernel, dim3(blocks), dim3(256), 0, st,
                        (uint8_t*)d_dst, nbytes, seed, first_word);
     BKD_HIP(hipGetLastError());
     return BKD_OK;

@@ -528,12 +528,14 @@ struct XPow8 {
 __global__ void __launch_bounds__(256) segments_combine_kernel(const uint32_t* __restrict__ seg_lengths,
                                                                const uint32_t* __restrict__ segcrc,
                                                                const uint64_t* __restrict__ first, uint64_t n,
-                                                               const uint32_t* __restrict__ seeds, uint32_t seed_all,
-                                                               XPow8 pw, uint32_t poly, uint32_t* __restrict__ out) {
+                                                               uint64_t nseg, const uint32_t* __restrict__ seeds,
+                                                               uint32_t seed_all, XPow8 pw, uint32_t poly,
+                                                               uint32_t* __restrict__ out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t reg = ~(seeds ? seeds[i] : seed_all);
-    const uint64_t k1 = first[i + 1];
+    // a malformed seg_first (decreasing or past nseg) is clamped: never a read past the segments
+    const uint64_t k1 = first[i + 1] < nseg ? first[i + 1] : nseg;
     for (uint64_t k = first[i]; k < k1; ++k) {
         uint32_t len = seg_lengths[k];
         if (!len) continue;  // ByteBufVisitor skips empty buffers (ByteBufVisitor.java:100-103,146-149)

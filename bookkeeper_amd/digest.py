@@ -162,22 +162,28 @@ class DigestManager:
 
     # ---- batch device path (new) ----
     def package_batch(self, entry_ids, lacs, length_fields, payload, offsets, lengths, frame_stride=None,
-                      stream=None):
+                      stream=None, sync_check: bool = False):
         """Frames n device-resident entries: returns (frames[n, frame_stride] uint8, digests int32[n]).
-        frames[i] = [32 B header][digest]; payload bytes stay where they are (ByteBufList(header, data))."""
+        frames[i] = [32 B header][digest]; payload bytes stay where they are (ByteBufList(header, data)).
+        An entry outside `payload` gets digest 0 and raises BKD_ERR_BOUNDS from the stream's next
+        bkd_stream_sync (here, when ``sync_check``)."""
         import torch
         n = offsets.numel()
         stride = frame_stride or (METADATA_LENGTH + self.macCodeLength)
         dev = payload.device
         frames = torch.empty((n, stride), dtype=torch.uint8, device=dev)
         digests = torch.empty(n, dtype=torch.int32, device=dev)
-        check(lib().bkd_digest_package_batch(
-            self.algo, self.ledgerId, _ck._dev_ptr(entry_ids, "entry_ids", torch.int64),
-            _ck._dev_ptr(lacs, "lacs", torch.int64), _ck._dev_ptr(length_fields, "length_fields", torch.int64),
-            _ck._dev_ptr(payload, "payload"), payload.numel() * payload.element_size(),
-            _ck._dev_ptr(offsets, "offsets", torch.int64), _ck._dev_ptr(lengths, "lengths", torch.int32), n,
-            _ck._dev_ptr(frames, "frames"), stride, _ck._dev_ptr(digests, "digests"),
-            _ck._stream_ptr(stream, payload)))
+        i64, u32 = torch.int64, _ck._u32_dtypes()
+        with _ck._on_device(payload):
+            st = _ck._stream_ptr(stream, payload)
+            check(lib().bkd_digest_package_batch(
+                self.algo, self.ledgerId, _ck._dev_ptr(entry_ids, "entry_ids", i64, dev, n),
+                _ck._dev_ptr(lacs, "lacs", i64, dev, n), _ck._dev_ptr(length_fields, "length_fields", i64, dev, n),
+                _ck._dev_ptr(payload, "payload"), payload.numel() * payload.element_size(),
+                _ck._dev_ptr(offsets, "offsets", i64, dev), _ck._dev_ptr(lengths, "lengths", u32, dev, n), n,
+                _ck._dev_ptr(frames, "frames"), stride, _ck._dev_ptr(digests, "digests"), st))
+            if sync_check:
+                check(lib().bkd_stream_sync(st))
         return frames, digests
 
     def verify_batch(self, framed, offsets, lengths, first_entry_id: int, skip_entry_check: bool = False,
@@ -189,12 +195,52 @@ class DigestManager:
         dev = framed.device
         status = torch.empty(n, dtype=torch.int32, device=dev)
         first_bad = torch.empty(1, dtype=torch.int64, device=dev)
-        check(lib().bkd_digest_verify_batch(
-            self.algo, self.ledgerId, first_entry_id, int(skip_entry_check), _ck._dev_ptr(framed, "framed"),
-            framed.numel() * framed.element_size(), _ck._dev_ptr(offsets, "offsets", torch.int64),
-            _ck._dev_ptr(lengths, "lengths", torch.int32), n, _ck._dev_ptr(status, "status"),
-            _ck._dev_ptr(first_bad, "first_bad"), _ck._stream_ptr(stream, framed)))
+        with _ck._on_device(framed):
+            check(lib().bkd_digest_verify_batch(
+                self.algo, self.ledgerId, first_entry_id, int(skip_entry_check), _ck._dev_ptr(framed, "framed"),
+                framed.numel() * framed.element_size(), _ck._dev_ptr(offsets, "offsets", torch.int64, dev),
+                _ck._dev_ptr(lengths, "lengths", _ck._u32_dtypes(), dev, n), n, _ck._dev_ptr(status, "status"),
+                _ck._dev_ptr(first_bad, "first_bad"), _ck._stream_ptr(stream, framed)))
         return status, first_bad
+
+    # ---- batch host path (new; entries in host memory, SURVEY §8f rows 1-2 / BASELINE config 5) ----
+    def verify_batch_host(self, frames, first_entry_id: int, skip_entry_check: bool = False):
+        """BatchedReadOp.complete over a ByteBufList (BatchedReadOp.java:164-190): `frames` is a
+        sequence of host buffers, each one framed entry. Returns (status int32[n], first_bad) with
+        first_bad = n when every entry verified, else the verified prefix's length."""
+        views = [_ck._host_view(f) for f in frames]
+        n = len(views)
+        ptrs = np.array([v.ctypes.data if v.size else 0 for v in views], dtype=np.uint64)
+        lens = np.array([v.size for v in views], dtype=np.uint32)
+        status = np.zeros(n, dtype=np.int32)
+        first_bad = ctypes.c_uint64(0)
+        check(lib().bkd_digest_verify_batch_host(
+            self.algo, self.ledgerId, first_entry_id, int(skip_entry_check), ctypes.c_void_p(ptrs.ctypes.data),
+            ctypes.c_void_p(lens.ctypes.data), n, ctypes.c_void_p(status.ctypes.data), ctypes.byref(first_bad)))
+        del views
+        return status, int(first_bad.value)
+
+    def package_batch_host(self, entry_ids, lacs, length_fields, payloads, frame_stride=None):
+        """PendingAddOp / LedgerFragmentReplicator packaging of host payloads (DigestManager.java:117-181)
+        in one call: returns (headers uint8[n, frame_stride] = [32 B header][digest], digests uint32[n])."""
+        views = [_ck._host_view(p) for p in payloads]
+        n = len(views)
+        stride = frame_stride or (METADATA_LENGTH + self.macCodeLength)
+        ids = np.ascontiguousarray(entry_ids, dtype=np.int64)
+        lac = np.ascontiguousarray(lacs, dtype=np.int64)
+        lf = np.ascontiguousarray(length_fields, dtype=np.int64)
+        if not (ids.size == lac.size == lf.size == n):
+            raise ValueError("entry_ids, lacs, length_fields and payloads must have one element per entry")
+        ptrs = np.array([v.ctypes.data if v.size else 0 for v in views], dtype=np.uint64)
+        lens = np.array([v.size for v in views], dtype=np.uint32)
+        frames = np.zeros((n, stride), dtype=np.uint8)
+        digests = np.zeros(n, dtype=np.uint32)
+        vp = ctypes.c_void_p
+        check(lib().bkd_digest_package_batch_host(
+            self.algo, self.ledgerId, vp(ids.ctypes.data), vp(lac.ctypes.data), vp(lf.ctypes.data),
+            vp(ptrs.ctypes.data), vp(lens.ctypes.data), n, vp(frames.ctypes.data), stride, vp(digests.ctypes.data)))
+        del views
+        return frames, digests
 
 
 class CRC32CDigestManager(DigestManager):
@@ -239,4 +285,4 @@ class DummyDigestManager(DigestManager):
     def package_batch(self, *a, **k):
         raise NotImplementedError("DUMMY digests need no device work")
 
-    verify_batch = package_batch
+    verify_batch = package_batch_host = verify_batch_host = package_batch

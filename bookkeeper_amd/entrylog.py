@@ -19,6 +19,8 @@ import numpy as np
 from . import checksum as _ck
 from ._native import CRC32, CRC32C, check, lib
 
+BKD_ERR_BOUNDS = -4
+
 LOGFILE_HEADER_SIZE = 1024  # DefaultEntryLogger.java:256
 INVALID_LID = -1            # DefaultEntryLogger.java:277
 
@@ -45,14 +47,22 @@ def scan_entry_log(log, start: int = LOGFILE_HEADER_SIZE) -> ScanResult:
     """DefaultEntryLogger.scanEntryLog (:995-1060) over a host buffer, accepting every ledger."""
     buf = _ck._host_view(log)
     size = buf.size
-    cap = max(1, size // 16)  # a record is at least 4 + 12 bytes (size field, ledger id, entry id)
-    offs = np.empty(cap, dtype=np.uint64)
-    lens = np.empty(cap, dtype=np.uint32)
-    lids = np.empty(cap, dtype=np.int64)
+    # a record takes at least 5 bytes (size field + 1 entry byte), so size // 5 + 1 always fits; start
+    # smaller (ledger entries are rarely tiny) and grow when the walk finds more records than that
+    cap = min(size // 5 + 1, max(64, size // 256))
     count = ctypes.c_uint64(0)
     end = ctypes.c_uint64(0)
-    check(lib().bkd_entrylog_index(buf.ctypes.data if size else None, size, start, offs.ctypes.data,
-                                   lens.ctypes.data, lids.ctypes.data, cap, ctypes.byref(count), ctypes.byref(end)))
+    while True:
+        offs = np.empty(cap, dtype=np.uint64)
+        lens = np.empty(cap, dtype=np.uint32)
+        lids = np.empty(cap, dtype=np.int64)
+        rc = lib().bkd_entrylog_index(buf.ctypes.data if size else None, size, start, offs.ctypes.data,
+                                      lens.ctypes.data, lids.ctypes.data, cap, ctypes.byref(count), ctypes.byref(end))
+        if rc == BKD_ERR_BOUNDS and cap < size // 5 + 1:
+            cap = min(size // 5 + 1, cap * 4)
+            continue
+        check(rc)
+        break
     k = int(count.value)
     return ScanResult(offs[:k].copy(), lens[:k].copy(), lids[:k].copy(), int(end.value))
 

@@ -20,10 +20,14 @@
  * Errors are return codes only (the reference native never throws, circe-checksum/pom.xml:87);
  * a human-readable message for the calling thread is available from bkd_last_error().
  * All entry points are thread-safe. Device-resident batch calls are asynchronous on the
- * caller's HIP stream (hipStream_t passed as void*, NULL = the null stream); buffers are
+ * caller's HIP stream (hipStream_t passed as void*, NULL = the null stream) and run on that
+ * stream's device (the calling thread's current device for the null stream); buffers are
  * borrowed only until the stream reaches the end of the call's work.
- * There is no CPU compute path: without a usable GPU the calls return BKD_ERR_NO_DEVICE
- * and the caller keeps its own CPU provider ($CJ/checksum/Crc32cIntChecksum.java:28-36 chain).
+ * Batch entry points always run on the GPU (BKD_ERR_NO_DEVICE without one). The per-call
+ * host-buffer resumes (bkd_resume / bkd_resume_host) take the library's own CPU route for
+ * buffers up to bkd_get_cpu_route_max() bytes and whenever no device is visible, so the
+ * provider never fails for lack of a GPU, as the reference's class-init selection never does
+ * ($CJ/checksum/Crc32cIntChecksum.java:28-36).
  */
 #ifndef BKDIGEST_H_
 #define BKDIGEST_H_
@@ -35,7 +39,12 @@
 extern "C" {
 #endif
 
-#define BKD_ABI_VERSION 1
+#define BKD_ABI_VERSION 2
+
+/* only the entry points below are exported (the library is built with -fvisibility=hidden) */
+#ifndef BKD_API
+#define BKD_API __attribute__((visibility("default")))
+#endif
 
 /* return codes */
 #define BKD_OK 0
@@ -57,20 +66,20 @@ extern "C" {
 #define BKD_VERIFY_LEDGER_MISMATCH 3 /* :267-273 */
 #define BKD_VERIFY_ENTRY_MISMATCH 4  /* :275-281 */
 
-int bkd_abi_version(void);
+BKD_API int bkd_abi_version(void);
 
 /* Number of visible HIP devices (0 when none). Replaces the capability probe
  * Sse42Crc32C.isSupported() -> nativeSupported() ($CJ/crc/Sse42Crc32C.java:31-47,
  * $CN/cpp/crc32c_sse42_jni.cpp:20-24). */
-int bkd_device_count(void);
+BKD_API int bkd_device_count(void);
 
 /* Uploads the CRC fold tables to `device` (idempotent, thread-safe). Replaces the
  * allocConfig chunk/shift-table construction ($CN/cpp/crc32c_sse42_jni.cpp:50-72,
  * $CN/cpp/crc32c_sse42.cpp:74-90). Optional: every call below initialises lazily. */
-int bkd_init(int device);
+BKD_API int bkd_init(int device);
 
 /* Message describing the last failure on the calling thread ("" if none). */
-const char* bkd_last_error(void);
+BKD_API const char* bkd_last_error(void);
 
 /* ---- device-resident batches: THE HOT PATH ---------------------------------------------
  * One CRC per entry, all entries in one launch. Entry i is the byte range
@@ -84,10 +93,10 @@ const char* bkd_last_error(void);
  * The indexed form checks offset+length <= base_size for every entry on the device and returns
  * BKD_ERR_BOUNDS from the NEXT synchronous call on this stream if any entry was out of range
  * (those entries get out = 0 and are not read). */
-int bkd_crc_batch_uniform(int algo, const void* d_base, uint64_t stride, uint32_t entry_len, uint64_t n,
+BKD_API int bkd_crc_batch_uniform(int algo, const void* d_base, uint64_t stride, uint32_t entry_len, uint64_t n,
                           const uint32_t* d_seeds, uint32_t seed_all, uint32_t* d_out, void* stream);
 
-int bkd_crc_batch(int algo, const void* d_base, uint64_t base_size, const uint64_t* d_offsets,
+BKD_API int bkd_crc_batch(int algo, const void* d_base, uint64_t base_size, const uint64_t* d_offsets,
                   const uint32_t* d_lengths, uint64_t n, const uint32_t* d_seeds, uint32_t seed_all,
                   uint32_t* d_out, void* stream);
 
@@ -99,26 +108,55 @@ int bkd_crc_batch(int algo, const void* d_base, uint64_t base_size, const uint64
  * without copying the pieces together. d_seg_first holds n + 1 non-decreasing indices
  * (d_seg_first[n] = nseg). Segments take the indexed path (bounds reported as for bkd_crc_batch);
  * one GF(2) combine per segment joins them. Device pointers; asynchronous on `stream`. */
-int bkd_crc_batch_segments(int algo, const void* d_base, uint64_t base_size, const uint64_t* d_seg_offsets,
+BKD_API int bkd_crc_batch_segments(int algo, const void* d_base, uint64_t base_size, const uint64_t* d_seg_offsets,
                            const uint32_t* d_seg_lengths, uint64_t nseg, const uint64_t* d_seg_first, uint64_t n,
                            const uint32_t* d_seeds, uint32_t seed_all, uint32_t* d_out, void* stream);
 
-/* Waits for `stream` and reports any bounds violation recorded by earlier indexed batches. */
-int bkd_stream_sync(void* stream);
+/* Waits for `stream` and reports (BKD_ERR_BOUNDS) any bounds violation recorded by the indexed
+ * batches enqueued on THIS stream since its previous bkd_stream_sync; the flag is per stream, so
+ * concurrent callers on other streams neither see nor clear it. */
+BKD_API int bkd_stream_sync(void* stream);
 
 /* ---- host-resident batches (the end-to-end path: Netty buffers in, digests out) -------
  * Synchronous. Copies the payload through pinned staging buffers with hipMemcpyAsync
  * (double-buffered H2D -> kernel -> D2H). Same semantics as bkd_crc_batch. */
-int bkd_crc_batch_host(int algo, const void* h_base, uint64_t base_size, const uint64_t* h_offsets,
+BKD_API int bkd_crc_batch_host(int algo, const void* h_base, uint64_t base_size, const uint64_t* h_offsets,
                        const uint32_t* h_lengths, uint64_t n, const uint32_t* h_seeds, uint32_t seed_all,
                        uint32_t* h_out);
 
 /* ---- per-call drop-in (IntHash.resume) ---------------------------------------------------
- * resume(current, ptr, len) for ONE buffer (host or device pointer), synchronous.
- * Replaces Sse42Crc32C.nativeUnsafe / nativeArray / nativeDirectBuffer
- * ($CN/cpp/crc32c_sse42_jni.cpp:26-48) and IntHash.resume ($CJ/checksum/IntHash.java:28-32).
- * Latency-bound by design (one launch per call); batch callers use bkd_crc_batch. */
-int bkd_resume(int algo, uint32_t current, const void* ptr, uint64_t len, uint32_t* out);
+ * resume(current, ptr, len) for ONE buffer, synchronous. Replaces Sse42Crc32C.nativeUnsafe /
+ * nativeArray / nativeDirectBuffer ($CN/cpp/crc32c_sse42_jni.cpp:26-48) and IntHash.resume
+ * ($CJ/checksum/IntHash.java:28-32). len == 0 returns `current` (crc32c_sse42.cpp:211-213).
+ *
+ * bkd_resume_host: a host buffer. Up to bkd_get_cpu_route_max() bytes, or with no device, the
+ *   CPU route (PCLMUL folding / SSE4.2 crc32, host_crc.cpp); above, the GPU through pinned staging.
+ * bkd_resume_device: a device buffer, on the caller's `stream` (ordered after the work that
+ *   produced the bytes), synchronous. One launch per call: batch callers use bkd_crc_batch.
+ * bkd_resume: either; the pointer kind is looked up (hipPointerGetAttributes), and a device
+ *   buffer runs on the null stream, which orders it after work on the blocking streams.
+ * bkd_cpu_resume: always the CPU route (no device needed). */
+BKD_API int bkd_resume(int algo, uint32_t current, const void* ptr, uint64_t len, uint32_t* out);
+BKD_API int bkd_resume_host(int algo, uint32_t current, const void* h_ptr, uint64_t len, uint32_t* out);
+BKD_API int bkd_resume_device(int algo, uint32_t current, const void* d_ptr, uint64_t len, void* stream,
+                              uint32_t* out);
+BKD_API int bkd_cpu_resume(int algo, uint32_t current, const void* h_ptr, uint64_t len, uint32_t* out);
+/* Host buffers up to this many bytes take the CPU route in bkd_resume / bkd_resume_host
+ * (0 = always the GPU when one is visible). Default from profiles/r02_call_latency.log. */
+BKD_API int bkd_set_cpu_route_max(uint64_t bytes);
+BKD_API uint64_t bkd_get_cpu_route_max(void);
+/* The CPU route's implementation on this host: "pclmul+sse4.2", "pclmul" or "slice8". */
+BKD_API const char* bkd_cpu_impl(void);
+
+/* ---- circe-checksum compatibility (the Sse42Crc32C natives, $CN/cpp/crc32c_sse42_jni.cpp) -----
+ * Backing for a drop-in libcirce-checksum.so (native/jni/bkdigest_jni.c). The chunk-word config
+ * only tunes the reference's SSE4.2 loop; results never depend on it, so it is validated and
+ * kept as an opaque handle. alloc: 0 unless len >= 1, every word >= 4 and the words strictly
+ * decrease (:50-72); free: releases a non-zero handle (:74-78). supported: 1 (the library
+ * always has a route: GPU or CPU), replacing nativeSupported (:20-24). */
+BKD_API int bkd_circe_supported(void);
+BKD_API int64_t bkd_circe_alloc_config(const int32_t* chunk_words, int32_t len);
+BKD_API void bkd_circe_free_config(int64_t config);
 
 /* ---- DigestManager batch framing (§8f rows 1-2) --------------------------------------
  * Package: for entry i with payload d_payload + d_offsets[i], d_lengths[i] bytes, write the
@@ -127,8 +165,9 @@ int bkd_resume(int algo, uint32_t current, const void* ptr, uint64_t len, uint32
  * (CRC32C: 4 B BE int, CRC32CDigestManager.java:44-46; CRC32: 8 B BE long zero-extended,
  * CRC32DigestManager.java:60-63) into d_frames + i*frame_stride (frame_stride >= 32 + mac).
  * digest = update(update(0, header), payload) (DigestManager.java:152-153, :177-178).
- * Device pointers; asynchronous on `stream`. */
-int bkd_digest_package_batch(int algo, int64_t ledger_id, const int64_t* d_entry_ids, const int64_t* d_lacs,
+ * Device pointers; asynchronous on `stream`. An out-of-range payload entry gets digest 0 and is
+ * reported by the next bkd_stream_sync on `stream` (BKD_ERR_BOUNDS). */
+BKD_API int bkd_digest_package_batch(int algo, int64_t ledger_id, const int64_t* d_entry_ids, const int64_t* d_lacs,
                              const int64_t* d_length_fields, const void* d_payload, uint64_t payload_size,
                              const uint64_t* d_offsets, const uint32_t* d_lengths, uint64_t n,
                              void* d_frames, uint64_t frame_stride, uint32_t* d_digests, void* stream);
@@ -139,10 +178,27 @@ int bkd_digest_package_batch(int algo, int64_t ledger_id, const int64_t* d_entry
  * ($BK/client/BatchedReadOp.java:164-190). expected entry id for entry i = first_entry_id + i
  * (DigestManager.verifyDigestAndReturnData(entryId, buf), :333-338); skip_entry_check mirrors
  * verifyDigest(buf) with skipEntryIdCheck (:206-208). Device pointers; asynchronous. */
-int bkd_digest_verify_batch(int algo, int64_t ledger_id, int64_t first_entry_id, int skip_entry_check,
+BKD_API int bkd_digest_verify_batch(int algo, int64_t ledger_id, int64_t first_entry_id, int skip_entry_check,
                             const void* d_framed, uint64_t framed_size, const uint64_t* d_offsets,
                             const uint32_t* d_lengths, uint64_t n, int32_t* d_status, uint64_t* d_first_bad,
                             void* stream);
+
+/* Host-resident framed batches (SURVEY §8f rows 1-2 with the entries in host memory, BASELINE
+ * config 5): entry i is its own host buffer h_frames[i] / h_payloads[i] of h_lengths[i] bytes,
+ * as BatchedReadOp's ByteBufList ($BK/client/BatchedReadOp.java:164-190) and PendingAddOp's
+ * payloads ($BK/client/PendingAddOp.java:261) hold them. The library gathers them into pinned
+ * staging (segments of <= 64 MiB, double-buffered, host copies on a thread pool), copies H2D,
+ * runs the device sequence of the device-resident call and copies the results back. Synchronous.
+ * verify: h_status[i] and *h_first_bad as bkd_digest_verify_batch (n if all verified).
+ * package: writes frame i's [32 B header][digest] to h_frames + i*frame_stride
+ * (32 + mac <= frame_stride <= 4096) and the digest value to h_digests[i]. */
+BKD_API int bkd_digest_verify_batch_host(int algo, int64_t ledger_id, int64_t first_entry_id, int skip_entry_check,
+                                         const void* const* h_frames, const uint32_t* h_lengths, uint64_t n,
+                                         int32_t* h_status, uint64_t* h_first_bad);
+BKD_API int bkd_digest_package_batch_host(int algo, int64_t ledger_id, const int64_t* h_entry_ids,
+                                          const int64_t* h_lacs, const int64_t* h_length_fields,
+                                          const void* const* h_payloads, const uint32_t* h_lengths, uint64_t n,
+                                          void* h_frames, uint64_t frame_stride, uint32_t* h_digests);
 
 /* ---- bookie-side entry-log scrub (§8f row 4) ------------------------------------------
  * An entry log is a 1024-byte file header (LOGFILE_HEADER_SIZE, DefaultEntryLogger.java:256)
@@ -155,7 +211,7 @@ int bkd_digest_verify_batch(int algo, int64_t ledger_id, int64_t first_entry_id,
  * entry's offset (first byte after the size field), length and ledger id; *h_end = the position
  * where the walk stopped. BKD_ERR_BOUNDS when more than `capacity` entries are found.
  * Host-only control logic: it reads 12 bytes per record and computes no digest. */
-int bkd_entrylog_index(const void* h_log, uint64_t log_size, uint64_t start, uint64_t* h_offsets,
+BKD_API int bkd_entrylog_index(const void* h_log, uint64_t log_size, uint64_t start, uint64_t* h_offsets,
                        uint32_t* h_lengths, int64_t* h_ledger_ids, uint64_t capacity, uint64_t* h_count,
                        uint64_t* h_end);
 
@@ -165,7 +221,7 @@ int bkd_entrylog_index(const void* h_log, uint64_t log_size, uint64_t start, uin
  * entry itself). Status codes as bkd_digest_verify_batch (0 ok, 1 too short, 2 digest mismatch);
  * *d_first_bad = first failing index or n. One digest type per call (the ledger's, from its
  * metadata). Asynchronous on `stream`; ragged batches go through the chunked plan. */
-int bkd_entrylog_verify(int algo, const void* d_log, uint64_t log_size, const uint64_t* d_offsets,
+BKD_API int bkd_entrylog_verify(int algo, const void* d_log, uint64_t log_size, const uint64_t* d_offsets,
                         const uint32_t* d_lengths, uint64_t n, int32_t* d_status, uint64_t* d_first_bad,
                         void* stream);
 
@@ -173,29 +229,29 @@ int bkd_entrylog_verify(int algo, const void* d_log, uint64_t log_size, const ui
 
 /* Fills nbytes of device memory with the little-endian splitmix64 stream
  * word_i = mix(seed + (first_word + i + 1) * 0x9E3779B97F4A7C15) (SURVEY.md §8d input definition). */
-int bkd_fill_splitmix64(void* d_dst, uint64_t nbytes, uint64_t seed, uint64_t first_word, void* stream);
+BKD_API int bkd_fill_splitmix64(void* d_dst, uint64_t nbytes, uint64_t seed, uint64_t first_word, void* stream);
 
 /* Host-only (no GPU needed): the compact fold-table image the kernels load into LDS for
  * `algo` and a group width of `lanes` (4, 8, 16, 32 or 64); returns words written or <0.
  * Layout documented in DESIGN.md §3. */
-int64_t bkd_host_tables(int algo, int lanes, uint32_t* out, uint64_t out_words);
+BKD_API int64_t bkd_host_tables(int algo, int lanes, uint32_t* out, uint64_t out_words);
 
 /* Host-only: GF(2) product a*b mod P in the reflected representation, and x^(8*nbytes) mod P. */
-uint32_t bkd_host_gf_mul(int algo, uint32_t a, uint32_t b);
-uint32_t bkd_host_xpow8n(int algo, uint64_t nbytes);
+BKD_API uint32_t bkd_host_gf_mul(int algo, uint32_t a, uint32_t b);
+BKD_API uint32_t bkd_host_xpow8n(int algo, uint64_t nbytes);
 
 /* Tuning: lanes per entry group (0 = automatic, else 1/4/8/16/32/64); prefetch is fixed at build. */
-int bkd_set_group_lanes(int lanes);
+BKD_API int bkd_set_group_lanes(int lanes);
 /* Indexed-batch strategy: 0 = automatic (chunked plan unless the base buffer is <= 256 KiB),
  * 1 = one entry per lane group, 2 = always the chunked plan. */
-int bkd_set_plan_mode(int mode);
+BKD_API int bkd_set_plan_mode(int mode);
 /* Chunked-plan geometry: lanes per group (4, 8, 16, 32 or 64), steps per full chunk (chunk = 16 * lanes *
  * steps bytes, <= 32 KiB) and the head-merge threshold in bytes (a head chunk shorter than this
  * joins its neighbour; >= 16). Default 8, 32, 16 (4 KiB chunks; tools/tune_plan.py). */
-int bkd_set_plan_geometry(int lanes, int steps_per_chunk, int merge_bytes);
+BKD_API int bkd_set_plan_geometry(int lanes, int steps_per_chunk, int merge_bytes);
 /* Register double-buffer depth of the plan's chunk kernel (2, 4 or 8 loads per lane). */
-int bkd_set_plan_prefetch(int loads_in_flight);
-int bkd_get_group_lanes(int algo, uint64_t mean_len);
+BKD_API int bkd_set_plan_prefetch(int loads_in_flight);
+BKD_API int bkd_get_group_lanes(int algo, uint64_t mean_len);
 
 #ifdef __cplusplus
 }

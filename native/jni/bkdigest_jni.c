@@ -1,0 +1,163 @@
+/*
+ * JNI shim over libbkdigest.so (include/bkdigest.h). Two Java classes bind to it:
+ *
+ * 1. com.scurrilous.circe.crc.Sse42Crc32C — the reference's own natives
+ *    (circe-checksum/src/main/circe/cpp/crc32c_sse42_jni.cpp:20-78; Java declarations at
+ *    circe-checksum/src/main/java/com/scurrilous/circe/crc/Sse42Crc32C.java:119-129), with the same
+ *    semantics, so an unmodified JVM that loads this library as /lib/libcirce-checksum.so picks the
+ *    engine up through JniIntHash (Crc32cIntChecksum.java:28-36):
+ *      nativeSupported          -> bkd_circe_supported (always 1: GPU or the library's CPU route)
+ *      nativeArray/DirectBuffer/Unsafe -> bkd_resume_host (host memory: CPU route up to
+ *                                  bkd_get_cpu_route_max() bytes, GPU above); a null direct-buffer
+ *                                  address returns 0 (:39-40); the config handle is ignored
+ *                                  (results never depend on the chunk ladder)
+ *      allocConfig / freeConfig -> bkd_circe_alloc_config / bkd_circe_free_config (same validation)
+ * 2. org.apache.bookkeeper.proto.checksum.GpuDigest — the batch surface the reference lacks
+ *    (INTEGRATION.md §2): device count/init, per-call resume for CRC32C and CRC32, host-memory
+ *    batches, and the host-resident DigestManager verify/package batches.
+ *
+ * Built only where a JDK is present (native/jni/Makefile; this image has none). Every C function it
+ * calls is exercised through ctypes in tests/ (test_native_host.py, test_gpu_*.py).
+ */
+#include <jni.h>
+#include <stdint.h>
+
+#include "bkdigest.h"
+
+/* ---- com.scurrilous.circe.crc.Sse42Crc32C ---------------------------------------------------- */
+
+JNIEXPORT jboolean JNICALL Java_com_scurrilous_circe_crc_Sse42Crc32C_nativeSupported(JNIEnv* env, jclass cls) {
+    (void)env;
+    (void)cls;
+    return bkd_circe_supported() ? JNI_TRUE : JNI_FALSE;
+}
+
+static jint resume_host_or_zero(jint current, const void* p, jlong length) {
+    uint32_t out = 0;
+    if (length <= 0) return current; /* crc32c_sse42.cpp:211-213 (the Java side rejects length < 0) */
+    return bkd_resume_host(BKD_CRC32C, (uint32_t)current, p, (uint64_t)length, &out) == BKD_OK ? (jint)out : 0;
+}
+
+JNIEXPORT jint JNICALL Java_com_scurrilous_circe_crc_Sse42Crc32C_nativeArray(JNIEnv* env, jclass cls, jint current,
+                                                                             jbyteArray input, jint index,
+                                                                             jint length, jlong config) {
+    (void)cls;
+    (void)config;
+    /* pinned for the duration of the call only, as crc32c_sse42_jni.cpp:29-31 */
+    jbyte* buf = (jbyte*)(*env)->GetPrimitiveArrayCritical(env, input, 0);
+    if (!buf) return 0;
+    const jint crc = resume_host_or_zero(current, buf + index, length);
+    (*env)->ReleasePrimitiveArrayCritical(env, input, buf, JNI_ABORT);
+    return crc;
+}
+
+JNIEXPORT jint JNICALL Java_com_scurrilous_circe_crc_Sse42Crc32C_nativeDirectBuffer(JNIEnv* env, jclass cls,
+                                                                                    jint current, jobject input,
+                                                                                    jint offset, jint length,
+                                                                                    jlong config) {
+    (void)cls;
+    (void)config;
+    const char* address = (const char*)(*env)->GetDirectBufferAddress(env, input);
+    if (!address) return 0; /* crc32c_sse42_jni.cpp:39-40 */
+    return resume_host_or_zero(current, address + offset, length);
+}
+
+JNIEXPORT jint JNICALL Java_com_scurrilous_circe_crc_Sse42Crc32C_nativeUnsafe(JNIEnv* env, jclass cls, jint current,
+                                                                              jlong address, jlong length,
+                                                                              jlong config) {
+    (void)env;
+    (void)cls;
+    (void)config;
+    return resume_host_or_zero(current, (const void*)(intptr_t)address, length);
+}
+
+JNIEXPORT jlong JNICALL Java_com_scurrilous_circe_crc_Sse42Crc32C_allocConfig(JNIEnv* env, jclass cls,
+                                                                              jintArray chunkWords) {
+    (void)cls;
+    const jsize len = (*env)->GetArrayLength(env, chunkWords);
+    jint* arr = (jint*)(*env)->GetPrimitiveArrayCritical(env, chunkWords, 0);
+    if (!arr) return 0;
+    const int64_t h = bkd_circe_alloc_config((const int32_t*)arr, (int32_t)len);
+    (*env)->ReleasePrimitiveArrayCritical(env, chunkWords, arr, JNI_ABORT);
+    return (jlong)h;
+}
+
+JNIEXPORT void JNICALL Java_com_scurrilous_circe_crc_Sse42Crc32C_freeConfig(JNIEnv* env, jclass cls, jlong config) {
+    (void)env;
+    (void)cls;
+    bkd_circe_free_config((int64_t)config);
+}
+
+/* ---- org.apache.bookkeeper.proto.checksum.GpuDigest (new batch surface) ---------------------- */
+
+JNIEXPORT jint JNICALL Java_org_apache_bookkeeper_proto_checksum_GpuDigest_deviceCount(JNIEnv* env, jclass cls) {
+    (void)env;
+    (void)cls;
+    return bkd_device_count();
+}
+
+JNIEXPORT jint JNICALL Java_org_apache_bookkeeper_proto_checksum_GpuDigest_init(JNIEnv* env, jclass cls, jint dev) {
+    (void)env;
+    (void)cls;
+    return bkd_init(dev);
+}
+
+/* resume(algo, current, address, length): a host address (Netty memoryAddress()); CRC32 included, for
+ * CRC32DigestManager's DirectMemoryCRC32Digest (CRC32DigestManager.java:28-87) */
+JNIEXPORT jint JNICALL Java_org_apache_bookkeeper_proto_checksum_GpuDigest_resumeAddress(JNIEnv* env, jclass cls,
+                                                                                       jint algo, jint current,
+                                                                                       jlong address, jlong len) {
+    (void)env;
+    (void)cls;
+    uint32_t out = 0;
+    if (len <= 0) return current;
+    if (!address) return 0;
+    return bkd_resume_host(algo, (uint32_t)current, (const void*)(intptr_t)address, (uint64_t)len, &out) == BKD_OK
+               ? (jint)out
+               : 0;
+}
+
+/* batch over one host region: offsets/lengths/seeds/out are addresses of direct buffers */
+JNIEXPORT jint JNICALL Java_org_apache_bookkeeper_proto_checksum_GpuDigest_resumeBatch(
+    JNIEnv* env, jclass cls, jint algo, jlong base, jlong size, jlong offs, jlong lens, jlong n, jlong seeds,
+    jint seedAll, jlong out) {
+    (void)env;
+    (void)cls;
+    return bkd_crc_batch_host(algo, (const void*)(intptr_t)base, (uint64_t)size, (const uint64_t*)(intptr_t)offs,
+                              (const uint32_t*)(intptr_t)lens, (uint64_t)n, (const uint32_t*)(intptr_t)seeds,
+                              (uint32_t)seedAll, (uint32_t*)(intptr_t)out);
+}
+
+/* BatchedReadOp.complete over a ByteBufList (BatchedReadOp.java:164-190): frame addresses and lengths
+ * in direct buffers; returns the verified prefix length (n if all verified) or a negative BKD_ERR_* */
+JNIEXPORT jlong JNICALL Java_org_apache_bookkeeper_proto_checksum_GpuDigest_verifyBatch(
+    JNIEnv* env, jclass cls, jint algo, jlong ledgerId, jlong firstEntryId, jboolean skipEntryIdCheck,
+    jlong frameAddrs, jlong frameLens, jlong n, jlong statusOut) {
+    (void)env;
+    (void)cls;
+    uint64_t first_bad = 0;
+    const int rc = bkd_digest_verify_batch_host(algo, ledgerId, firstEntryId, skipEntryIdCheck ? 1 : 0,
+                                                (const void* const*)(intptr_t)frameAddrs,
+                                                (const uint32_t*)(intptr_t)frameLens, (uint64_t)n,
+                                                (int32_t*)(intptr_t)statusOut, &first_bad);
+    return rc == BKD_OK ? (jlong)first_bad : (jlong)rc;
+}
+
+/* PendingAddOp / LedgerFragmentReplicator packaging (DigestManager.java:117-181) of n host payloads */
+JNIEXPORT jint JNICALL Java_org_apache_bookkeeper_proto_checksum_GpuDigest_packageBatch(
+    JNIEnv* env, jclass cls, jint algo, jlong ledgerId, jlong entryIds, jlong lacs, jlong lengthFields,
+    jlong payloadAddrs, jlong payloadLens, jlong n, jlong framesOut, jlong frameStride, jlong digestsOut) {
+    (void)env;
+    (void)cls;
+    return bkd_digest_package_batch_host(algo, ledgerId, (const int64_t*)(intptr_t)entryIds,
+                                         (const int64_t*)(intptr_t)lacs, (const int64_t*)(intptr_t)lengthFields,
+                                         (const void* const*)(intptr_t)payloadAddrs,
+                                         (const uint32_t*)(intptr_t)payloadLens, (uint64_t)n,
+                                         (void*)(intptr_t)framesOut, (uint64_t)frameStride,
+                                         (uint32_t*)(intptr_t)digestsOut);
+}
+
+JNIEXPORT jstring JNICALL Java_org_apache_bookkeeper_proto_checksum_GpuDigest_lastError(JNIEnv* env, jclass cls) {
+    (void)cls;
+    return (*env)->NewStringUTF(env, bkd_last_error());
+}

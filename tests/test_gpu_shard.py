@@ -1,0 +1,136 @@
+"""GPU: the full-size per-GPU workloads of BASELINE configs 2 and 4 against the reference, and the
+N > 1 path run for real — two rank processes calling libbkdigest on the device (gloo for the
+bookkeeping collectives; one GPU here, so both ranks share it), and bench.py starting its own ranks.
+
+Config 4 = 64M x 4 KiB entries split evenly over 8 GPUs; rank r's shard is entries
+[r*8M, (r+1)*8M) of ONE global splitmix64 stream (bench.shard_first_word). The test runs rank 7's
+shard (32 GiB) on this GPU: every digest through the uniform kernel equals the indexed path's, and
+equals the reference's circe crc32c() (oracle/_ref, threaded) on the host copy when that was built,
+else a 20 000-entry sample of the C oracle."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle
+from bench import shard_first_word
+from bookkeeper_amd import checksum as ck
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _reference_or_sample(host: np.ndarray, entry_len: int, n: int, got: np.ndarray):
+    ref = oracle.ref()
+    if ref is not None:
+        want = np.zeros(n, dtype=np.uint32)
+        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+        ref.ref_crc32c_uniform_timed(host.ctypes.data_as(oracle._u8p), entry_len, entry_len, n, threads, 1,
+                                     want.ctypes.data_as(oracle._u32p))
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, f"{bad.size} digests differ from the reference, first at {bad[:5]}"
+        return "reference, every entry"
+    idx = np.random.default_rng(3).choice(n, 20000, replace=False)
+    for i in idx:
+        assert got[i] == oracle.calculate(0, host[i * entry_len:(i + 1) * entry_len]), i
+    return "oracle sample"
+
+
+def test_config2_full_batch_vs_reference(gpu):
+    """BASELINE config 2: all 1M x 4 KiB digests against the reference (not a self-comparison)."""
+    import torch
+    n, L = 1 << 20, 4096
+    base = torch.empty(n * L, dtype=torch.uint8, device=gpu)
+    ck.fill_splitmix64(base, 42)
+    got = ck.crc_batch_uniform(ck.CRC32C, base, L, n).cpu().numpy().view(np.uint32)
+    host = base.cpu().numpy()
+    _reference_or_sample(host, L, n, got)
+
+
+def test_config4_rank7_shard_8m(gpu):
+    import torch
+    n, L, rank = 8 << 20, 4096, 7
+    base = torch.empty(n * L, dtype=torch.uint8, device=gpu)
+    ck.fill_splitmix64(base, 42, first_word=shard_first_word(rank, n, L))
+    got_u = ck.crc_batch_uniform(ck.CRC32C, base, L, n)
+    offs = torch.arange(n, dtype=torch.int64, device=gpu) * L
+    lens = torch.full((n,), L, dtype=torch.int32, device=gpu)
+    got_i = ck.crc_batch(ck.CRC32C, base, offs, lens, sync_check=True)
+    assert torch.equal(got_u, got_i)
+    del offs, lens, got_i
+    got = got_u.cpu().numpy().view(np.uint32)
+    host = base.cpu().numpy()
+    del base
+    torch.cuda.empty_cache()
+    # the shard really is rank 7's slice of the global stream: its first words are the global ones
+    assert (host[:4096] == oracle.fill_splitmix64(4096, 42, shard_first_word(rank, n, L))).all()
+    _reference_or_sample(host, L, n, got)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+_RANK_SCRIPT = r"""
+import os, sys
+sys.path.insert(0, {root!r})
+import numpy as np, torch, torch.distributed as dist
+from bench import shard_first_word
+from bookkeeper_amd import checksum as ck
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+dist.init_process_group("gloo", rank=rank, world_size=world)
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+n, L = {n}, 4096
+base = torch.empty(n * L, dtype=torch.uint8, device=dev)
+ck.fill_splitmix64(base, 42, first_word=shard_first_word(rank, n, L))
+out = ck.crc_batch_uniform(ck.CRC32C, base, L, n).cpu().to(torch.int64)
+parts = [torch.zeros(n, dtype=torch.int64) for _ in range(world)]
+dist.all_gather(parts, out)
+if rank == 0:
+    np.save({path!r}, torch.cat(parts).numpy().astype(np.uint32))
+dist.destroy_process_group()
+"""
+
+
+def test_two_rank_processes_shard_through_libbkdigest(gpu, tmp_path):
+    """The N > 1 data path for real: two rank processes, each digesting its shard through the HIP
+    library; the gathered digests equal the oracle's over the unsharded stream."""
+    n, world = 8192, 2
+    path = str(tmp_path / "digests.npy")
+    script = _RANK_SCRIPT.format(root=ROOT, n=n, path=path)
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-c", script], env=env))
+    for p in procs:
+        assert p.wait(timeout=240) == 0
+    got = np.load(path)
+    whole = oracle.fill_splitmix64(world * n * 4096, 42)
+    want = oracle.uniform(0, whole, 4096, 4096, world * n)
+    assert (got == want).all()
+
+
+def test_bench_self_launches_ranks(gpu):
+    """bench.py --gpus 2 outside torch.distributed.run starts its own two ranks (gloo here, both on
+    this GPU) and rank 0 reports n_gpus 2 with per-GPU numbers."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--entries",
+           "65536", "--steps", "5", "--warmup", "2", "--no-cpu-baseline"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["n_gpus"] == 2 and res["scaling"] == "weak"
+    assert len(res["per_gpu"]) == 2 and all(p["GiB_s"] > 0 and p["solo_GiB_s"] > 0 for p in res["per_gpu"])
+    assert 0 < res["efficiency_vs_solo"] < 2

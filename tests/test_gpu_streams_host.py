@@ -1,0 +1,235 @@
+"""GPU: per-stream bounds reporting, stream-ordered per-call resumes, the CPU/GPU per-call routes,
+and the host-resident DigestManager batches (BatchedReadOp / PendingAddOp with entries in host
+memory), all bit-exact against the oracle."""
+import threading
+
+import numpy as np
+import pytest
+
+import oracle
+from bookkeeper_amd import checksum as ck
+from bookkeeper_amd import digest as dg
+from bookkeeper_amd._native import BkdError, lib
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(torch, a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def test_bounds_flag_is_per_stream(gpu):
+    """include/bkdigest.h: an out-of-range entry is reported by bkd_stream_sync of the stream it was
+    enqueued on, and only there (one flag per stream, read and cleared in stream order)."""
+    import torch
+    rng = np.random.default_rng(5)
+    size = 1 << 20
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    base = _dev(torch, host, gpu)
+    n = 5000
+    offs = rng.integers(0, size - 4096, n).astype(np.int64)
+    lens = rng.integers(0, 4096, n).astype(np.int32)
+    bad_offs = offs.copy()
+    bad_offs[1234] = size - 10  # 10 bytes left, entry wants more
+    lens_bad = lens.copy()
+    lens_bad[1234] = 4000
+    want = oracle.batch(0, host, offs.astype(np.uint64), lens.astype(np.uint32))
+    results = {}
+    barrier = threading.Barrier(2)
+
+    def worker(name, o, l):
+        s = torch.cuda.Stream(device=gpu)
+        d_off, d_len = _dev(torch, o, gpu), _dev(torch, l, gpu)
+        torch.cuda.synchronize()
+        barrier.wait()
+        try:
+            for _ in range(20):
+                out = ck.crc_batch(0, base, d_off, d_len, stream=s)
+            ck.check(lib().bkd_stream_sync(ck._stream_ptr(s)))
+            results[name] = ("ok", out.cpu().numpy().view(np.uint32))
+        except BkdError as e:
+            results[name] = ("err", e.code)
+
+    for mode in (1, 2):  # direct kernel and chunked plan both raise the flag
+        ck.set_plan_mode(mode)
+        ts = [threading.Thread(target=worker, args=("bad", bad_offs, lens_bad)),
+              threading.Thread(target=worker, args=("good", offs, lens))]
+        try:
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join(timeout=120)
+        finally:
+            ck.set_plan_mode(0)
+        assert results["bad"] == ("err", -4), mode
+        assert results["good"][0] == "ok", mode
+        assert (results["good"][1] == want).all()
+    # the flag was cleared by the sync that reported it
+    s = torch.cuda.Stream(device=gpu)
+    ck.crc_batch(0, base, _dev(torch, offs, gpu), _dev(torch, lens, gpu), stream=s, sync_check=True)
+
+
+def test_resume_device_is_ordered_after_the_producer(gpu):
+    """a per-call resume of a tensor written by a still-queued kernel must see the
+    new bytes. The producer is queued behind a long matmul on the current stream; no explicit sync."""
+    import torch
+    h = ck.GpuIntHash(ck.CRC32C)
+    a = torch.randn(4096, 4096, device=gpu)
+    for trial in range(3):
+        buf = torch.zeros(1 << 20, dtype=torch.uint8, device=gpu)
+        torch.cuda.synchronize()
+        for _ in range(4):
+            a = a @ a  # keep the stream busy
+            a = a / a.abs().max()
+        buf.fill_(0x5A + trial)  # the producer, queued after the matmuls
+        got = h.calculate(buf)
+        want = oracle.calculate(0, np.full(1 << 20, 0x5A + trial, dtype=np.uint8))
+        assert got & 0xFFFFFFFF == want, trial
+    # a side stream producer with the resume on that stream
+    s = torch.cuda.Stream(device=gpu)
+    with torch.cuda.stream(s):
+        buf2 = torch.full((70000,), 7, dtype=torch.uint8, device=gpu)
+        for _ in range(2):
+            a = a @ a
+        buf2.add_(1)
+        got = h.calculate(buf2)
+    assert got & 0xFFFFFFFF == oracle.calculate(0, np.full(70000, 8, dtype=np.uint8))
+
+
+@pytest.mark.parametrize("algo", [ck.CRC32C, ck.CRC32])
+def test_per_call_routes_agree(gpu, algo):
+    """bkd_resume_host: CPU route (<= cpu_route_max) and GPU route (threshold 0) give the oracle's
+    value; bkd_resume (pointer lookup) on host and device buffers too."""
+    import ctypes
+    import torch
+    rng = np.random.default_rng(11 + algo)
+    h = ck.GpuIntHash(algo)
+    old = ck.get_cpu_route_max()
+    try:
+        for n in (1, 15, 16, 63, 64, 100, 4096, 65537, 1 << 20, (3 << 20) + 5):
+            data = rng.integers(0, 256, n, dtype=np.uint8)
+            seed = int(rng.integers(0, 2**32))
+            want = oracle.resume(algo, seed, data)
+            for route_max in (0, 1 << 62):  # 0: GPU via pinned staging; huge: CPU
+                ck.set_cpu_route_max(route_max)
+                assert h.resume(seed, data) & 0xFFFFFFFF == want, (n, route_max)
+                out = ctypes.c_uint32(0)
+                ck.check(lib().bkd_resume(algo, seed, ctypes.c_void_p(data.ctypes.data), n, ctypes.byref(out)))
+                assert out.value == want
+            d = _dev(torch, data, gpu)
+            assert h.resume(seed, d) & 0xFFFFFFFF == want
+            out = ctypes.c_uint32(0)
+            ck.check(lib().bkd_resume(algo, seed, ctypes.c_void_p(d.data_ptr()), n, ctypes.byref(out)))
+            assert out.value == want
+    finally:
+        ck.set_cpu_route_max(old)
+
+
+def test_package_batch_reports_out_of_range_payload(gpu):
+    import torch
+    dm = dg.DigestManager.instantiate(3, b"", dg.DigestType.CRC32C)
+    n = 64
+    payload = torch.zeros(n * 100, dtype=torch.uint8, device=gpu)
+    ids = torch.arange(n, dtype=torch.int64, device=gpu)
+    offs = ids * 100
+    lens = torch.full((n,), 100, dtype=torch.int32, device=gpu)
+    dm.package_batch(ids, ids - 1, ids, payload, offs, lens, sync_check=True)
+    lens[n - 1] = 101  # one byte past the payload buffer
+    with pytest.raises(BkdError) as e:
+        dm.package_batch(ids, ids - 1, ids, payload, offs, lens, sync_check=True)
+    assert e.value.code == -4
+
+
+def test_batch_wrappers_validate_out_and_seeds(gpu):
+    import torch
+    base = torch.zeros(4096, dtype=torch.uint8, device=gpu)
+    offs = torch.zeros(8, dtype=torch.int64, device=gpu)
+    lens = torch.full((8,), 16, dtype=torch.int32, device=gpu)
+    with pytest.raises(ValueError):
+        ck.crc_batch(0, base, offs, lens, out=torch.empty(4, dtype=torch.int32, device=gpu))
+    with pytest.raises(TypeError):
+        ck.crc_batch(0, base, offs, lens, seeds=torch.zeros(8, dtype=torch.int64, device=gpu))
+    with pytest.raises(TypeError):
+        ck.crc_batch_uniform(0, base, 16, 8, out=torch.empty(8, dtype=torch.int64, device=gpu))
+    with pytest.raises(ValueError):
+        ck.crc_batch_uniform(0, base, 16, 8, seeds=torch.zeros(4, dtype=torch.int32, device=gpu))
+
+
+def _frames(algo, rng, n, ledger, first_id, max_payload):
+    frames = []
+    for i in range(n):
+        size = int(rng.choice([0, 1, 5, 31, 100, 4096 - 36, int(rng.integers(0, max_payload))]))
+        payload = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
+        digest, hdr = oracle.digest_entry(algo, ledger, first_id + i, first_id + i - 1, size, payload)
+        frames.append(bytearray(hdr + oracle.digest_bytes(algo, digest) + payload))
+    return frames
+
+
+@pytest.mark.parametrize("algo,dtype", [(ck.CRC32C, dg.DigestType.CRC32C), (ck.CRC32, dg.DigestType.CRC32)])
+def test_verify_batch_host_matches_oracle(gpu, algo, dtype):
+    """BatchedReadOp.complete (BatchedReadOp.java:164-190) over a ByteBufList in host memory: every
+    entry's status equals oracle.verify_entry's, first_bad is the verified prefix."""
+    rng = np.random.default_rng(21 + algo)
+    ledger, first = 99, 1000
+    dm = dg.DigestManager.instantiate(ledger, b"", dtype)
+    frames = _frames(algo, rng, 3000, ledger, first, 9000)
+    st, fb = dm.verify_batch_host(frames, first)
+    assert (st == 0).all() and fb == len(frames)
+    # corruptions: payload byte, digest byte, ledger id, entry id, truncated frame
+    frames[2500][-1 if len(frames[2500]) > 40 + dm.macCodeLength else 33] ^= 0x40
+    frames[1700][32] ^= 1
+    frames[2100][7] ^= 1  # ledger id (BE, last byte)
+    frames[2900][15] ^= 1  # entry id
+    frames[2950] = frames[2950][:20]
+    st, fb = dm.verify_batch_host(frames, first)
+    want = np.array([oracle.verify_entry(algo, bytes(f), ledger, first + i) for i, f in enumerate(frames)])
+    assert (st == want).all()
+    assert fb == 1700
+    st, fb = dm.verify_batch_host(frames[:1700], first)
+    assert fb == 1700 and (st == 0).all()
+
+
+def test_verify_batch_host_many_segments(gpu):
+    """> 64 MiB of frames: several double-buffered segments; the first bad entry in a later segment."""
+    algo = ck.CRC32C
+    n, L = 40000, 4096  # ~156 MiB
+    ledger = 5
+    dm = dg.DigestManager.instantiate(ledger, b"", dg.DigestType.CRC32C)
+    big = oracle.fill_splitmix64(n * L, 42).reshape(n, L)
+    plen = L - 36
+    for i in range(n):
+        d, hdr = oracle.digest_entry(algo, ledger, i, i - 1, plen, big[i, 36:])
+        big[i, :32] = np.frombuffer(hdr, dtype=np.uint8)
+        big[i, 32:36] = np.frombuffer(oracle.digest_bytes(algo, d), dtype=np.uint8)
+    frames = [big[i] for i in range(n)]
+    st, fb = dm.verify_batch_host(frames, 0)
+    assert fb == n and (st == 0).all()
+    big[31000, 2000] ^= 0xFF
+    big[39999, 100] ^= 0xFF
+    st, fb = dm.verify_batch_host(frames, 0)
+    assert fb == 31000
+    assert set(np.nonzero(st)[0].tolist()) == {31000, 39999}
+
+
+@pytest.mark.parametrize("algo,dtype", [(ck.CRC32C, dg.DigestType.CRC32C), (ck.CRC32, dg.DigestType.CRC32)])
+@pytest.mark.parametrize("stride", [None, 64])
+def test_package_batch_host_matches_oracle(gpu, algo, dtype, stride):
+    """PendingAddOp's packaging (DigestManager.java:117-181) of host payloads in one call: header and
+    digest bytes equal oracle.digest_entry's for every entry, across several segments."""
+    rng = np.random.default_rng(31 + algo)
+    ledger = 12345
+    dm = dg.DigestManager.instantiate(ledger, b"", dtype)
+    n = 20000
+    sizes = rng.choice([0, 1, 17, 1000, 4060, 9000], n)
+    sizes[-5:] = 70000
+    payloads = [rng.integers(0, 256, int(s), dtype=np.uint8) for s in sizes]
+    ids = np.arange(n, dtype=np.int64) + 77
+    lacs = ids - 1
+    lf = np.cumsum(sizes).astype(np.int64)
+    frames, digests = dm.package_batch_host(ids, lacs, lf, payloads, frame_stride=stride)
+    mac = dm.macCodeLength
+    for i in range(0, n, 7):
+        d, hdr = oracle.digest_entry(algo, ledger, int(ids[i]), int(lacs[i]), int(lf[i]), payloads[i])
+        assert digests[i] == d, i
+        assert bytes(frames[i, :32]) == hdr
+        assert bytes(frames[i, 32:32 + mac]) == oracle.digest_bytes(algo, d)

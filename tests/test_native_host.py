@@ -1,6 +1,8 @@
-"""CPU: the C-ABI library loads and exports every symbol include/bkdigest.h declares; its
-host-side operator tables are right; and the kernel's decomposition (modelled in Python
-with the library's own tables) reproduces the oracle bit-exactly. No GPU compute here."""
+"""CPU: the C-ABI library loads and exports every symbol include/bkdigest.h declares (and no other
+C symbol); its host-side operator tables are right; its per-call CPU route (host_crc.cpp) matches the
+golden fixtures and the oracle; the circe-compat config helpers keep the reference's validation; and
+the kernel's decomposition (modelled in Python with the library's own tables) reproduces the oracle
+bit-exactly. No GPU compute here."""
 import ctypes
 import subprocess
 
@@ -24,7 +26,9 @@ def test_library_exports_every_declared_symbol():
     dyn = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True).stdout
     exported = {line.split()[-1] for line in dyn.splitlines() if " T " in line}
     assert set(declared) <= exported
-    assert L.bkd_abi_version() == 1
+    # nothing but the declared entry points leaks as a C symbol (C++ kernel stubs are mangled)
+    assert {x for x in exported if not x.startswith("_Z") and not x.startswith("__hip")} == set(declared)
+    assert L.bkd_abi_version() == 2
 
 
 def test_library_contains_gfx950_code():
@@ -32,14 +36,81 @@ def test_library_contains_gfx950_code():
     assert b"amdgcn-amd-amdhsa--gfx950" in blob  # offload bundle entry id for the gfx950 code object
 
 
-def test_no_device_is_an_error_not_a_fallback():
+def test_no_device_per_call_takes_cpu_route_batches_fail_loudly():
+    """Crc32cIntChecksum.java:28-36 never throws: with no device the per-call resume is served by the
+    library's own CPU route; batch entry points still refuse to run (no silent CPU batch path)."""
     if _native.device_count() > 0:
         pytest.skip("a device is visible")
+    L = _native.lib()
     out = ctypes.c_uint32(0)
-    rc = _native.lib().bkd_resume(0, 0, b"123456789", 9, ctypes.byref(out))
-    assert rc == -2  # BKD_ERR_NO_DEVICE: no silent CPU path
+    for fn in (L.bkd_resume, L.bkd_resume_host):
+        assert fn(0, 0, b"123456789", 9, ctypes.byref(out)) == 0
+        assert out.value == 0xE3069283  # CRCTest.java:133-135
+    assert ck.GpuIntHash().calculate(b"123456789") == ck.to_java_int(0xE3069283)
+    assert ck.Crc32cIntChecksum.computeChecksum(b"Some String") == 608512271  # ChecksumTest.java:41
+    # above the CPU-route threshold too: no device means the CPU route whatever the size
+    big = np.arange(3 << 20, dtype=np.uint32).view(np.uint8)
+    assert ck.GpuIntHash().calculate(big) == ck.to_java_int(oracle.calculate(0, big))
+    offs = np.zeros(1, dtype=np.uint64)
+    lens = np.full(1, 9, dtype=np.uint32)
+    res = np.zeros(1, dtype=np.uint32)
+    rc = L.bkd_crc_batch_host(0, b"123456789", 9, offs.ctypes.data, lens.ctypes.data, 1, None, 0, res.ctypes.data)
+    assert rc == -2  # BKD_ERR_NO_DEVICE: batches are GPU work
     with pytest.raises(_native.BkdError):
-        ck.GpuIntHash().calculate(b"123456789")
+        ck.crc_batch_host(0, b"123456789", offs, lens)
+
+
+@pytest.mark.parametrize("algo", [0, 1])
+def test_cpu_route_against_golden_and_oracle(algo):
+    """host_crc.cpp (PCLMUL folding / crc32q / slice-by-8) vs the reference-generated fixtures, and
+    vs the oracle on every length 0..600, lengths around its fold thresholds, and random seeds and
+    alignments."""
+    import golden_util
+    key = "crc32c" if algo == 0 else "crc32"
+    for v in golden_util.load()["literal"]:
+        assert ck.cpu_resume(algo, 0, golden_util.literal_bytes(v)) & 0xFFFFFFFF == int(v[key], 16), v["name"]
+    fx = golden_util.load()["batch"]
+    data = oracle.fill_splitmix64(fx["bytes"], fx["seed"])
+    for i, (o, n, sd) in enumerate(zip(fx["offsets"], fx["lengths"], fx["seeds"])):
+        got = ck.cpu_resume(algo, int(sd, 16), data[o:o + n]) & 0xFFFFFFFF
+        assert got == int(fx[key][i], 16), i
+    rng = np.random.default_rng(77 + algo)
+    buf = rng.integers(0, 256, 1 << 17, dtype=np.uint8)
+    lengths = list(range(0, 601)) + [1023, 1024, 1025, 4095, 4096, 4097, 65535, 65536, 100000]
+    for n in lengths:
+        off = int(rng.integers(0, 64))
+        seed = int(rng.integers(0, 2**32))
+        want = oracle.resume(algo, seed, buf[off:off + n])
+        assert ck.cpu_resume(algo, seed, buf[off:off + n]) & 0xFFFFFFFF == want, n
+    assert ck.cpu_impl() in ("pclmul+sse4.2", "pclmul", "slice8")
+
+
+def test_cpu_route_threshold_setting():
+    old = ck.get_cpu_route_max()
+    try:
+        ck.set_cpu_route_max(12345)
+        assert ck.get_cpu_route_max() == 12345
+    finally:
+        ck.set_cpu_route_max(old)
+
+
+def test_circe_config_compat():
+    """Sse42Crc32C.allocConfig validation (crc32c_sse42_jni.cpp:50-72): >= 1 word, every word >= 4
+    (chunk_config::min_words), strictly decreasing; 0 on failure, an opaque non-zero handle otherwise."""
+    L = _native.lib()
+
+    def alloc(words):
+        a = np.array(words, dtype=np.int32)
+        return L.bkd_circe_alloc_config(ctypes.c_void_p(a.ctypes.data if a.size else 0), a.size)
+
+    assert L.bkd_circe_supported() == 1
+    for bad in ([], [3], [4096, 4096], [64, 512], [4096, 512, 3], [-1]):
+        assert alloc(bad) == 0, bad
+    for good in ([4], [4096, 512, 64], [64, 4]):
+        h = alloc(good)
+        assert h != 0
+        L.bkd_circe_free_config(h)
+    L.bkd_circe_free_config(0)  # freeing the null config is a no-op, as delete[] of null
 
 
 @pytest.mark.parametrize("algo", [0, 1])
