@@ -82,6 +82,7 @@ PROTOTYPES = {
     "bkd_set_plan_mode": (_int, [_int]),
     "bkd_set_plan_geometry": (_int, [_int, _int, _int]),
     "bkd_set_plan_prefetch": (_int, [_int]),
+    "bkd_set_plan_small": (_int, [_u32]),
     "bkd_get_group_lanes": (_int, [_int, _u64]),
 }
 

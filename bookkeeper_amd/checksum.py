@@ -311,6 +311,11 @@ def set_plan_mode(mode: int) -> None:
     check(lib().bkd_set_plan_mode(mode))
 
 
+def set_plan_small(max_bytes: int = 192) -> None:
+    """Entries of <= max_bytes of a planned indexed batch run in the short-entry launch (0 = none)."""
+    check(lib().bkd_set_plan_small(max_bytes))
+
+
 def set_plan_prefetch(loads_in_flight: int = 2) -> None:
     check(lib().bkd_set_plan_prefetch(loads_in_flight))
 

@@ -6,6 +6,7 @@
 // entry point runs on the GPU and returns BKD_ERR_NO_DEVICE without one.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -65,6 +66,21 @@ struct StreamScratch {
     // only); read and cleared in stream order. h_err: pinned landing word for the read.
     uint32_t* err = nullptr;
     uint32_t* h_err = nullptr;
+    // PlanRun word of the plans enqueued on this stream and the epoch of the latest one
+    uint32_t* run = nullptr;
+    uint32_t epoch = 0;
+    hipError_t run_word(hipStream_t st, uint32_t** out) {
+        if (!run) {
+            hipError_t e = hipMallocAsync((void**)&run, sizeof(uint32_t), st);
+            if (e == hipSuccess) e = hipMemsetAsync(run, 0, sizeof(uint32_t), st);
+            if (e != hipSuccess) {
+                run = nullptr;
+                return e;
+            }
+        }
+        *out = run;
+        return hipSuccess;
+    }
     hipError_t flag(hipStream_t st, uint32_t** out) {
         if (!err) {
             hipError_t e = hipMallocAsync((void**)&err, sizeof(uint32_t), st);
@@ -129,6 +145,12 @@ std::atomic<int> g_plan_lanes{8};
 std::atomic<int> g_plan_jc{32};
 std::atomic<int> g_plan_merge{16};
 std::atomic<int> g_plan_pf{2};  // loads in flight per lane in the chunk kernel (2, 4 or 8)
+// Short-entry class of indexed batches: entries of <= this many bytes skip the plan and run in
+// their own launch (4-lane groups, next entry loaded during the current one). 0 = none.
+constexpr int kSmallLanes = 4;
+constexpr uint32_t kSmallMaxBytes = 16u * kSmallLanes * 3u;  // one register set per entry (PF = 2)
+std::atomic<uint32_t> g_plan_small{kSmallMaxBytes};
+constexpr uint64_t kShortClassMeanMax = 1024;  // bytes of base buffer per entry
 // Indexed batches whose base buffer is at most this size skip the plan (latency over balance).
 constexpr uint64_t kDirectMaxBytes = 256u << 10;
 
@@ -299,25 +321,26 @@ int dispatch_lanes(DeviceState& ds, int lanes, int algo, const uint8_t* base, co
 }
 
 template <int G>
-void launch_plan_chunks(const uint8_t* base, const bkd::PlanDesc* descs, const uint32_t* count, const uint32_t* tab,
+void launch_plan_chunks(const uint32_t* run_flag, uint32_t run_epoch, const uint8_t* base, const bkd::PlanDesc* descs,
+                        const uint32_t* count, const uint32_t* tab,
                         uint32_t* out, uint32_t* partials, const bkd::PlanDirectSrc& ov, int blocks, hipStream_t st) {
     const int pf = g_plan_pf.load();
     if (pf == 8)
         hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 8, kNT, bkd::PlanDirectSrc>), dim3((unsigned)blocks),
-                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov);
+                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run_flag, run_epoch);
     else if (pf == 4)
         hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 4, kNT, bkd::PlanDirectSrc>), dim3((unsigned)blocks),
-                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov);
+                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run_flag, run_epoch);
     else
         hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 2, kNT, bkd::PlanDirectSrc>), dim3((unsigned)blocks),
-                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov);
+                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run_flag, run_epoch);
 }
 
 // Indexed batch through the chunked plan (plan_kernels.hpp): five stream-ordered kernels, no
 // host sync, scratch from the stream's arena.
 int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, const uint64_t* offsets,
                 const uint32_t* lengths, uint64_t n, const uint32_t* seeds, uint32_t seed_all, uint32_t* out,
-                hipStream_t st) {
+                hipStream_t st, bool short_class = true) {
     if (n == 0) return BKD_OK;
     if (n >= 0xFFFFFFF0ull) return fail(BKD_ERR_INVALID_ARG, "indexed batches hold fewer than 2^32 - 16 entries");
     const int G = g_plan_lanes.load();
@@ -330,6 +353,11 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     pg.nbins = (pg.ch + pg.merge - 1u + pg.step - 1u) / pg.step + 1u;
     pg.step_sh = (uint32_t)__builtin_ctz(pg.step);
     pg.ch_sh = (pg.ch & (pg.ch - 1u)) == 0u ? (uint32_t)__builtin_ctz(pg.ch) : 0xFFu;
+    // The short-entry launch walks every entry's index in rounds of one entry per 4-lane group, a
+    // memory round trip each: it pays where short entries dominate (64 M x 64 B: 7.2 -> 1.9 ms) and
+    // costs more than it saves where they are a minority of a large-entry batch (config 3's Zipf:
+    // +54 us launch, -43 us chunk kernel). So it runs when the mean entry is at most 1 KiB.
+    pg.small = (short_class && size <= (uint64_t)kShortClassMeanMax * n) ? g_plan_small.load() : 0u;
     const uint32_t* xtab = nullptr;
     int rc = xtab_for(ds, algo, pg.ch, &xtab);
     if (rc) return rc;
@@ -338,7 +366,7 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     const uint32_t nb = (uint32_t)((n + bkd::kPlanBlock - 1) / bkd::kPlanBlock);
     const uint32_t ncols = pg.nbins + 1u;
     Carver cv;
-    const size_t o_blk = cv.take((size_t)nb * ncols * 4),
+    const size_t o_blk = cv.take((size_t)nb * ncols * 4), o_live = cv.take((size_t)nb * 4),
                  o_blkoff = cv.take((size_t)nb * ncols * 4), o_hdr = cv.take(bkd::kHdrWords * 4),
                  o_ps = cv.take((size_t)n * 4), o_part = cv.take((size_t)capacity * 4),
                  o_desc = cv.take((size_t)capacity * sizeof(bkd::PlanDesc));
@@ -346,33 +374,54 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     std::lock_guard<std::recursive_mutex> lk(sc.mu);
     uint8_t* sb = nullptr;
     uint32_t* err = nullptr;
+    uint32_t* run_word = nullptr;
     hipError_t e = sc.get(0, cv.used, st, &sb);
     if (e == hipSuccess) e = sc.flag(st, &err);
+    if (e == hipSuccess && pg.small) e = sc.run_word(st, &run_word);
     if (e != hipSuccess) return fail(BKD_ERR_NOMEM, std::string("plan scratch: ") + hipGetErrorString(e));
-    uint32_t *blk = Carver::at<uint32_t>(sb, o_blk),
+    // with a short-entry class the plan kernels run only if that launch met one of their entries
+    bkd::PlanRun run{nullptr, 0u};
+    if (pg.small) {
+        if (++sc.epoch == 0u) ++sc.epoch;  // 0 is the word's initial value
+        run = bkd::PlanRun{run_word, sc.epoch};
+    }
+    uint32_t *blk = Carver::at<uint32_t>(sb, o_blk), *blive = Carver::at<uint32_t>(sb, o_live),
              *blkoff = Carver::at<uint32_t>(sb, o_blkoff), *hdr = Carver::at<uint32_t>(sb, o_hdr),
              *pslot = Carver::at<uint32_t>(sb, o_ps), *partials = Carver::at<uint32_t>(sb, o_part);
     bkd::PlanDesc* descs = Carver::at<bkd::PlanDesc>(sb, o_desc);
-    hipLaunchKernelGGL(bkd::plan_count_kernel, dim3(nb), dim3(bkd::kPlanBlock), 0, st, offsets, lengths, size, n, pg,
-                       blk);
-    hipLaunchKernelGGL(bkd::plan_scan_kernel, dim3(ncols), dim3(64), 0, st, blk, nb, blkoff, hdr);
+    if (pg.small) {  // the short-entry class, in its own launch (any order against the plan kernels)
+        const bkd::SmallIndexedSrc ss{n, offsets, lengths, seeds, seed_all, size, out, pg.small, run_word, run.epoch};
+        const uint64_t per_block = bkd::kBlock / kSmallLanes;
+        const unsigned sblocks = (unsigned)std::min<uint64_t>((n + per_block - 1) / per_block, (uint64_t)ds.cus);
+        hipLaunchKernelGGL((bkd::crc_groups_kernel<kSmallLanes, 2, kNT, bkd::SmallIndexedSrc>), dim3(sblocks),
+                           dim3(bkd::kBlock), 0, st, base, ss, ds.tables[algo][lane_index(kSmallLanes)], err);
+    }
+    // count / emit / combine walk their 1024-entry blocks in grid stride (BKD_PLAN_GRID blocks per CU;
+    // 0: one block per entry block)
+#ifndef BKD_PLAN_GRID
+#define BKD_PLAN_GRID 2
+#endif
+    const uint32_t pgrid = BKD_PLAN_GRID ? (uint32_t)BKD_PLAN_GRID * (uint32_t)ds.cus : 0xFFFFFFFFu;
+    hipLaunchKernelGGL(bkd::plan_count_kernel, dim3(std::min(nb, pgrid)), dim3(bkd::kPlanBlock), 0, st, offsets,
+                       lengths, size, n, pg, blk, blive, nb, run);
+    hipLaunchKernelGGL(bkd::plan_scan_kernel, dim3(ncols), dim3(bkd::kPlanBlock), 0, st, blk, nb, blkoff, hdr, run);
     // few entry blocks (large entries): replicate emit and combine blocks so ~2 blocks per CU work
     const uint32_t reps = nb >= 2u * (uint32_t)ds.cus ? 1u : std::min<uint32_t>(64u, (2u * (uint32_t)ds.cus + nb - 1u) / nb);
-    hipLaunchKernelGGL(bkd::plan_emit_kernel, dim3(nb * reps), dim3(bkd::kPlanBlock), 0, st, offsets, lengths, seeds,
-                       seed_all, size, n, pg, capacity, blkoff, pslot, hdr, descs, reps);
+    hipLaunchKernelGGL(bkd::plan_emit_kernel, dim3(std::min(nb * reps, pgrid)), dim3(bkd::kPlanBlock), 0, st, offsets,
+                       lengths, seeds, seed_all, size, n, pg, capacity, blkoff, pslot, hdr, descs, reps, blive, nb, run);
     const uint32_t* tab = ds.tables[algo][lane_index(G)];
     const bkd::PlanDirectSrc ov{n, offsets, lengths, seeds, seed_all, size, out, pslot, hdr, capacity};
     switch (G) {
-        case 4: launch_plan_chunks<4>(base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st); break;
-        case 8: launch_plan_chunks<8>(base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st); break;
-        case 16: launch_plan_chunks<16>(base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st); break;
-        case 32: launch_plan_chunks<32>(base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st); break;
-        default: launch_plan_chunks<64>(base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st); break;
+        case 4: launch_plan_chunks<4>(run.flag, run.epoch, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st); break;
+        case 8: launch_plan_chunks<8>(run.flag, run.epoch, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st); break;
+        case 16: launch_plan_chunks<16>(run.flag, run.epoch, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st); break;
+        case 32: launch_plan_chunks<32>(run.flag, run.epoch, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st); break;
+        default: launch_plan_chunks<64>(run.flag, run.epoch, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st); break;
     }
     const uint32_t* btab = tab + bkd::gf2::byte_table_offset(G);
-    hipLaunchKernelGGL(bkd::plan_combine_kernel, dim3(nb * reps), dim3(1024), 0, st, base, offsets, lengths, seeds,
+    hipLaunchKernelGGL(bkd::plan_combine_kernel, dim3(std::min(nb * reps, pgrid)), dim3(1024), 0, st, base, offsets, lengths, seeds,
                        seed_all, size, n, pg, xtab, bkd::gf2::xpow(algo, 8ull * pg.ch), tab + 1024, btab, ds.xinv[algo],
-                       bkd::gf2::poly(algo), pslot, partials, out, err, reps);
+                       bkd::gf2::poly(algo), pslot, partials, out, err, reps, blive, nb, run);
     e = hipGetLastError();
     if (e != hipSuccess) return fail(BKD_ERR_HIP, std::string("plan kernels: ") + hipGetErrorString(e));
     return BKD_OK;
@@ -862,7 +911,7 @@ int resume_device(int algo, uint32_t current, const void* ptr, uint64_t len, hip
         c->h_out[1] = l32;
         const hipError_t e = hipMemcpyAsync(c->d_len, c->h_out + 1, 4, hipMemcpyHostToDevice, st);
         rc = e == hipSuccess ? launch_plan(*ds, algo, (const uint8_t*)ptr, len, c->d_off, c->d_len, 1, nullptr,
-                                           current, c->d_out, st)
+                                           current, c->d_out, st, false)
                              : fail(BKD_ERR_HIP, hipGetErrorString(e));
     }
     if (!rc) {
@@ -923,6 +972,13 @@ int bkd_set_plan_geometry(int lanes, int steps_per_chunk, int merge_bytes) {
     g_plan_lanes.store(lanes);
     g_plan_jc.store(steps_per_chunk);
     g_plan_merge.store(merge_bytes);
+    return BKD_OK;
+}
+
+int bkd_set_plan_small(uint32_t max_bytes) {
+    if (max_bytes > kSmallMaxBytes || (max_bytes && max_bytes < 16u))
+        return fail(BKD_ERR_INVALID_ARG, "short-entry class bound must be 0 or 16.." + std::to_string(kSmallMaxBytes));
+    g_plan_small.store(max_bytes);
     return BKD_OK;
 }
 

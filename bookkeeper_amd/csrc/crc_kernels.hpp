@@ -55,22 +55,37 @@ __device__ __forceinline__ uint32_t lds_word(const uint32_t* lds, uint32_t byte_
     return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + byte_addr);
 }
 
+// a ^ b ^ c in one v_bitop3_b32 (gfx950; truth table 0x96), for the compact-table products.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
 // v * C_main via the replicated tables. lanereg = 4*(lane&31) | 1<<16.
 // v_perm_b32 result bytes (b3..b0) = (0, hi, v.byte_t, 4*(lane&31)); hi = 1 selects the
 // upper 64 KiB half (tables 2, 3); the +128 immediate selects the odd table of a pair.
-__device__ __forceinline__ uint32_t mul_main(const uint32_t* lds, uint32_t v, uint32_t lanereg) {
+// mul_main_add(.., d) = v * C_main ^ d.
+__device__ __forceinline__ uint32_t mul_main_add(const uint32_t* lds, uint32_t v, uint32_t lanereg, uint32_t d) {
     const uint32_t a0 = __builtin_amdgcn_perm(v, lanereg, 0x0C0C0400u);
     const uint32_t a1 = __builtin_amdgcn_perm(v, lanereg, 0x0C0C0500u);
     const uint32_t a2 = __builtin_amdgcn_perm(v, lanereg, 0x0C020600u);
     const uint32_t a3 = __builtin_amdgcn_perm(v, lanereg, 0x0C020700u);
-    return lds_word(lds, a0) ^ lds_word(lds, a1 + 128u) ^ lds_word(lds, a2) ^ lds_word(lds, a3 + 128u);
+    // plain XORs: consumed in issue order (a v_bitop3 here measured up to 10 % slower on short entries)
+    return lds_word(lds, a0) ^ lds_word(lds, a1 + 128u) ^ lds_word(lds, a2) ^ lds_word(lds, a3 + 128u) ^ d;
+}
+
+__device__ __forceinline__ uint32_t mul_main(const uint32_t* lds, uint32_t v, uint32_t lanereg) {
+    return mul_main_add(lds, v, lanereg, 0u);
 }
 
 // v * C via a compact 4x256 operator set at LDS byte offset `off`.
+__device__ __forceinline__ uint32_t mul_aux_add(const uint32_t* lds, uint32_t off, uint32_t v, uint32_t d) {
+    return xor3(xor3(lds_word(lds, off + ((v & 0xffu) << 2)), lds_word(lds, off + 1024u + (((v >> 8) & 0xffu) << 2)),
+                     lds_word(lds, off + 2048u + (((v >> 16) & 0xffu) << 2))),
+                lds_word(lds, off + 3072u + ((v >> 24) << 2)), d);
+}
+
 __device__ __forceinline__ uint32_t mul_aux(const uint32_t* lds, uint32_t off, uint32_t v) {
-    return lds_word(lds, off + ((v & 0xffu) << 2)) ^ lds_word(lds, off + 1024u + (((v >> 8) & 0xffu) << 2)) ^
-           lds_word(lds, off + 2048u + (((v >> 16) & 0xffu) << 2)) ^
-           lds_word(lds, off + 3072u + ((v >> 24) << 2));
+    return mul_aux_add(lds, off, v, 0u);
 }
 
 template <bool NT>
@@ -183,6 +198,23 @@ struct FramedPayloadSrc {
     }
 };
 
+// Indexed entries of at most `small` bytes (small <= 16*G*(PF+1)): the short-entry class of a
+// ragged batch, run by its own launch (indexed_small_loop) while the chunked plan takes the rest
+// (plan_kernels.hpp, PlanGeo::small). Longer entries are skipped here.
+struct SmallIndexedSrc {
+    uint64_t n;
+    const uint64_t* offsets;
+    const uint32_t* lengths;
+    const uint32_t* seeds;
+    uint32_t seed_all;
+    uint64_t size;
+    uint32_t* out;
+    uint32_t small;
+    uint32_t* plan_flag;  // set to plan_epoch when an entry of the plan's is met (PlanRun)
+    uint32_t plan_epoch;
+    __device__ __forceinline__ uint64_t count() const { return n; }
+};
+
 // DPP row_shl:SH — lane i receives lane i + SH of its 16-lane row (0 past the row end).
 template <int SH>
 __device__ __forceinline__ uint32_t dpp_row_shl(uint32_t v) {
@@ -198,7 +230,7 @@ __device__ __forceinline__ uint32_t lane_tree_dpp(const uint32_t* lds, uint32_t 
         return v;
     } else {
         const uint32_t other = dpp_row_shl<(1 << LV)>(v);
-        v = mul_aux(lds, x32_off + 4096u * (uint32_t)(1 + LV), v) ^ other;
+        v = mul_aux_add(lds, x32_off + 4096u * (uint32_t)(1 + LV), v, other);
         return lane_tree_dpp<LV + 1, LEVELS>(lds, x32_off, v);
     }
 }
@@ -216,20 +248,20 @@ __device__ __forceinline__ uint32_t finish_lanes(const uint32_t* lds, uint32_t c
     if constexpr (G == 1) {
         // one lane per entry: x^128 is the main operator itself (replicated, conflict-free); no tree
         const uint32_t lanereg = ((uint32_t)(threadIdx.x & 31) << 2) | (1u << 16);
-        return mul_main(lds, c0, lanereg) ^ mul_aux(lds, Gm::kX96Off, c1) ^ mul_aux(lds, Gm::kX64Off, c2) ^
-               mul_aux(lds, Gm::kX32Off, c3);
+        return mul_main_add(lds, c0, lanereg,
+                            mul_aux_add(lds, Gm::kX96Off, c1, mul_aux_add(lds, Gm::kX64Off, c2, mul_aux(lds, Gm::kX32Off, c3))));
     } else if constexpr (Gm::kFast) {
-        const uint32_t v = mul_aux(lds, Gm::kX32Off + 4096u, c0) ^ mul_aux(lds, Gm::kX96Off, c1) ^
-                           mul_aux(lds, Gm::kX64Off, c2) ^ mul_aux(lds, Gm::kX32Off, c3);
+        const uint32_t v = xor3(mul_aux(lds, Gm::kX32Off + 4096u, c0), mul_aux(lds, Gm::kX96Off, c1),
+                                mul_aux_add(lds, Gm::kX64Off, c2, mul_aux(lds, Gm::kX32Off, c3)));
         return lane_tree_dpp<0, Gm::kLevels>(lds, Gm::kX32Off, v);
     } else {
-        uint32_t v = mul_aux(lds, Gm::kX32Off, c0) ^ c1;
-        v = mul_aux(lds, Gm::kX32Off, v) ^ c2;
-        v = mul_aux(lds, Gm::kX32Off, v) ^ c3;
+        uint32_t v = mul_aux_add(lds, Gm::kX32Off, c0, c1);
+        v = mul_aux_add(lds, Gm::kX32Off, v, c2);
+        v = mul_aux_add(lds, Gm::kX32Off, v, c3);
 #pragma unroll
         for (int lv = 0; lv < Gm::kLevels; ++lv) {
             const uint32_t other = (uint32_t)__shfl_xor((int)v, 1 << lv);
-            v = mul_aux(lds, Gm::kX32Off + 4096u * (uint32_t)(1 + lv), v) ^ other;
+            v = mul_aux_add(lds, Gm::kX32Off + 4096u * (uint32_t)(1 + lv), v, other);
         }
         return mul_aux(lds, Gm::kX32Off, v);
     }
@@ -302,18 +334,18 @@ __device__ __forceinline__ uint32_t fold_range(const uint32_t* lds, uint32_t lan
     const uint32_t rem = J - 1u;
 #define BKD_FOLD0(d)                                     \
     do {                                                 \
-        c0 = mul_main(lds, c0, lanereg) ^ (d).x ^ fx;    \
+        c0 = mul_main_add(lds, c0, lanereg, (d).x ^ fx);    \
         fx = 0u;                                         \
-        c1 = mul_main(lds, c1, lanereg) ^ (d).y;         \
-        c2 = mul_main(lds, c2, lanereg) ^ (d).z;         \
-        c3 = mul_main(lds, c3, lanereg) ^ (d).w;         \
+        c1 = mul_main_add(lds, c1, lanereg, (d).y);         \
+        c2 = mul_main_add(lds, c2, lanereg, (d).z);         \
+        c3 = mul_main_add(lds, c3, lanereg, (d).w);         \
     } while (0)
 #define BKD_FOLD(d)                                  \
     do {                                             \
-        c0 = mul_main(lds, c0, lanereg) ^ (d).x;     \
-        c1 = mul_main(lds, c1, lanereg) ^ (d).y;     \
-        c2 = mul_main(lds, c2, lanereg) ^ (d).z;     \
-        c3 = mul_main(lds, c3, lanereg) ^ (d).w;     \
+        c0 = mul_main_add(lds, c0, lanereg, (d).x);     \
+        c1 = mul_main_add(lds, c1, lanereg, (d).y);     \
+        c2 = mul_main_add(lds, c2, lanereg, (d).z);     \
+        c3 = mul_main_add(lds, c3, lanereg, (d).w);     \
     } while (0)
     if (rem >= (uint32_t)PF) {
         // A/B register double buffer: fold one block while the other block's loads fly.
@@ -403,6 +435,8 @@ struct SmallGeo {
     int64_t s, a, la0;  // entry start, this lane's step-0 block, its load address (>= s, in bounds)
     uint32_t J;
     uint32_t r0;
+    uint32_t len;
+    int kind;  // indexed entries: 0 fold, 1 shorter than 16 B (serial), 2 out of bounds, 3 the plan's, 4 none
 };
 
 template <int G>
@@ -416,6 +450,58 @@ __device__ __forceinline__ SmallGeo small_geo(const UniformSrc& src, uint64_t i,
     return c;
 }
 
+// One entry's index words, loaded a round before its data (no dependent index -> data chain).
+struct SmallIdx {
+    uint64_t o;
+    uint32_t l;
+    uint32_t seed;
+};
+
+__device__ __forceinline__ SmallIdx small_idx(const SmallIndexedSrc& src, uint64_t i) {
+    SmallIdx x;
+    if (i < src.n) {
+        x.o = src.offsets[i];
+        x.l = src.lengths[i];
+        x.seed = src.seeds ? src.seeds[i] : src.seed_all;
+    } else {
+        x.o = ~0ull;  // past the batch
+        x.l = 0xFFFFFFFFu;
+        x.seed = 0u;
+    }
+    return x;
+}
+
+template <int G>
+__device__ __forceinline__ SmallGeo small_geo(const SmallIndexedSrc& src, const SmallIdx& x, int g) {
+    SmallGeo c;
+    c.len = x.l;
+    c.kind = 3;
+    c.s = c.a = c.la0 = 0;  // entries not folded here load base[0, 16) (the plan runs only on >= 256 KiB bases)
+    c.J = 1;
+    c.r0 = 0u;
+    if (x.o == ~0ull) {
+        c.kind = 4;  // past the batch
+    } else if (c.len <= src.small) {
+        const uint64_t o = x.o;
+        if (o > src.size || (uint64_t)c.len > src.size - o) {
+            c.kind = 2;
+        } else {
+            c.r0 = ~x.seed;
+            if (c.len < 16u) {
+                c.kind = 1;
+                c.s = (int64_t)o;
+            } else {
+                c.kind = 0;
+                c.s = (int64_t)o;
+                c.J = (c.len + (uint32_t)Geo<G>::kStep - 1u) / (uint32_t)Geo<G>::kStep;
+                c.a = c.s + (int64_t)c.len - (int64_t)c.J * Geo<G>::kStep + 16 * g;
+                c.la0 = c.a >= c.s ? c.a : c.s;
+            }
+        }
+    }
+    return c;
+}
+
 template <int G, int PF, bool NT>
 __device__ __forceinline__ void small_load(const uint8_t* __restrict__ base, const SmallGeo& c, u32x4& W0,
                                            u32x4 (&A)[PF]) {
@@ -425,6 +511,18 @@ __device__ __forceinline__ void small_load(const uint8_t* __restrict__ base, con
         const int64_t addr = (uint32_t)(k + 1) < c.J ? c.a + (int64_t)(k + 1) * Geo<G>::kStep : c.la0;
         A[k] = ld16<NT>(base + addr);
     }
+}
+
+// small_load for the indexed class: only the entry's own steps (J of them) and nothing for entries
+// not folded here — no duplicate requests for 1-step entries, none for skipped ones.
+template <int G, int PF, bool NT>
+__device__ __forceinline__ void small_load_exact(const uint8_t* __restrict__ base, const SmallGeo& c, u32x4& W0,
+                                                 u32x4 (&A)[PF]) {
+    if (c.kind != 0) return;
+    W0 = ld16<NT>(base + c.la0);
+#pragma unroll
+    for (int k = 0; k < PF; ++k)
+        if ((uint32_t)(k + 1) < c.J) A[k] = ld16<NT>(base + c.a + (int64_t)(k + 1) * Geo<G>::kStep);
 }
 
 // Raw register of a short entry from its loaded blocks (fold_range's arithmetic, J <= PF + 1).
@@ -451,10 +549,10 @@ __device__ __forceinline__ uint32_t small_fold(const uint32_t* lds, uint32_t lan
 #pragma unroll
     for (int k = 0; k < PF; ++k) {
         if ((uint32_t)(k + 1) < c.J) {
-            c0 = mul_main(lds, c0, lanereg) ^ A[k].x ^ (k == 0 ? fx : 0u);
-            c1 = mul_main(lds, c1, lanereg) ^ A[k].y;
-            c2 = mul_main(lds, c2, lanereg) ^ A[k].z;
-            c3 = mul_main(lds, c3, lanereg) ^ A[k].w;
+            c0 = mul_main_add(lds, c0, lanereg, A[k].x ^ (k == 0 ? fx : 0u));
+            c1 = mul_main_add(lds, c1, lanereg, A[k].y);
+            c2 = mul_main_add(lds, c2, lanereg, A[k].z);
+            c3 = mul_main_add(lds, c3, lanereg, A[k].w);
         }
     }
     return finish_lanes<G>(lds, c0, c1, c2, c3);
@@ -490,6 +588,67 @@ __device__ __forceinline__ void uniform_small_loop(const uint32_t* lds, uint32_t
     }
 }
 
+// The short-entry class of an indexed batch (SmallIndexedSrc), with uniform_small_loop's X/Y
+// lookahead: a group's next entry is loaded while the current one folds. Entries of other kinds
+// take their branch (serial bytes, bounds error, skip) without loads of their own.
+// Returns whether this lane met an entry of the plan's (kind 3).
+template <int G, int PF, bool NT>
+__device__ __forceinline__ bool indexed_small_loop(const uint32_t* lds, uint32_t lanereg, int g,
+                                                   const uint8_t* __restrict__ base, const SmallIndexedSrc& src,
+                                                   uint64_t n, uint64_t gid, uint64_t ngroups,
+                                                   uint32_t* __restrict__ err) {
+    using Gm = Geo<G>;
+    bool saw_plan = false;
+    auto finish = [&](const SmallGeo& c, uint64_t i, const u32x4& W0, const u32x4(&A)[PF]) {
+        saw_plan |= c.kind == 3;
+        if (c.kind == 0) {
+            const uint32_t v = small_fold<G, PF>(lds, lanereg, c, W0, A);
+            if (g == 0) src.out[i] = ~v;
+        } else if (c.kind == 1) {  // < 16 B: serial byte loop (ReflectedIntCrc.java:44-48 form)
+            if (g == 0) {
+                uint32_t r = c.r0;
+                const uint8_t* q = base + c.s;
+                for (uint32_t k = 0; k < c.len; ++k)
+                    r = lds_word(lds, Gm::kByteTabOff + (((r ^ q[k]) & 0xffu) << 2)) ^ (r >> 8);
+                src.out[i] = ~r;
+            }
+        } else if (c.kind == 2) {
+            if (g == 0) {
+                src.out[i] = 0u;
+                if (err) atomicOr(err, 1u);
+            }
+        }
+    };
+    // index words two entries ahead, data one entry ahead (X/Y register sets)
+    u32x4 W0x, Ax[PF], W0y, Ay[PF];
+    SmallGeo cx = small_geo<G>(src, small_idx(src, gid), g), cy;
+    SmallIdx nx = small_idx(src, gid + ngroups);
+    small_load_exact<G, PF, NT>(base, cx, W0x, Ax);
+    for (uint64_t i = gid;;) {
+        uint64_t j = i + ngroups;
+        SmallIdx nn = small_idx(src, j + ngroups);
+        if (j < n) {
+            cy = small_geo<G>(src, nx, g);
+            small_load_exact<G, PF, NT>(base, cy, W0y, Ay);
+        }
+        finish(cx, i, W0x, Ax);
+        if (j >= n) break;
+        i = j;
+        nx = nn;
+        j = i + ngroups;
+        nn = small_idx(src, j + ngroups);
+        if (j < n) {
+            cx = small_geo<G>(src, nx, g);
+            small_load_exact<G, PF, NT>(base, cx, W0x, Ax);
+        }
+        finish(cy, i, W0y, Ay);
+        if (j >= n) break;
+        i = j;
+        nx = nn;
+    }
+    return saw_plan;
+}
+
 // One CRC per work item of `src` (uniform / indexed / framed-payload entries), persistent grid.
 template <int G, int PF, bool NT, class Src>
 __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __restrict__ base, Src src,
@@ -512,7 +671,13 @@ __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __res
             return;
         }
     }
-    groups_loop<G, PF, NT>(lds, lanereg, g, base, src, n, gid, ngroups, err);
+    if constexpr (std::is_same<Src, SmallIndexedSrc>::value) {
+        bool saw = false;
+        if (gid < n) saw = indexed_small_loop<G, PF, NT>(lds, lanereg, g, base, src, n, gid, ngroups, err);
+        if (__any(saw) && (threadIdx.x & 63) == 0 && src.plan_flag) *src.plan_flag = src.plan_epoch;
+    } else {
+        groups_loop<G, PF, NT>(lds, lanereg, g, base, src, n, gid, ngroups, err);
+    }
 }
 
 // ---- chunk descriptors of the ragged-batch plan (built by plan_kernels.hpp) ----
@@ -564,14 +729,22 @@ __device__ __forceinline__ ChunkGeo chunk_geo(const PlanDesc& d, int g) {
 }
 
 // Loads of step 0 and steps 1..PF of chunk c (addresses past the chunk clamp to a valid block).
+#ifndef BKD_PF_SKIP
+#define BKD_PF_SKIP 0
+#endif
 template <int G, int PF, bool NT>
 __device__ __forceinline__ void chunk_prefetch(const uint8_t* __restrict__ base, const ChunkGeo& c, u32x4& W0,
                                                u32x4 (&A)[PF]) {
     W0 = ld16<NT>(base + c.la0);
 #pragma unroll
     for (int k = 0; k < PF; ++k) {
-        const int64_t addr = (uint32_t)(k + 1) < c.J ? c.a + (int64_t)(k + 1) * Geo<G>::kStep : c.la0;
-        A[k] = ld16<NT>(base + addr);
+        if constexpr (BKD_PF_SKIP) {
+            // steps past the chunk are not loaded at all (no duplicate requests for short chunks)
+            if ((uint32_t)(k + 1) < c.J) A[k] = ld16<NT>(base + c.a + (int64_t)(k + 1) * Geo<G>::kStep);
+        } else {
+            const int64_t addr = (uint32_t)(k + 1) < c.J ? c.a + (int64_t)(k + 1) * Geo<G>::kStep : c.la0;
+            A[k] = ld16<NT>(base + addr);
+        }
     }
 }
 
@@ -602,18 +775,18 @@ __device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lan
     const uint32_t rem = c.J - 1u;
 #define BKD_FOLD0(d)                                     \
     do {                                                 \
-        c0 = mul_main(lds, c0, lanereg) ^ (d).x ^ fx;    \
+        c0 = mul_main_add(lds, c0, lanereg, (d).x ^ fx);    \
         fx = 0u;                                         \
-        c1 = mul_main(lds, c1, lanereg) ^ (d).y;         \
-        c2 = mul_main(lds, c2, lanereg) ^ (d).z;         \
-        c3 = mul_main(lds, c3, lanereg) ^ (d).w;         \
+        c1 = mul_main_add(lds, c1, lanereg, (d).y);         \
+        c2 = mul_main_add(lds, c2, lanereg, (d).z);         \
+        c3 = mul_main_add(lds, c3, lanereg, (d).w);         \
     } while (0)
 #define BKD_FOLD(d)                                  \
     do {                                             \
-        c0 = mul_main(lds, c0, lanereg) ^ (d).x;     \
-        c1 = mul_main(lds, c1, lanereg) ^ (d).y;     \
-        c2 = mul_main(lds, c2, lanereg) ^ (d).z;     \
-        c3 = mul_main(lds, c3, lanereg) ^ (d).w;     \
+        c0 = mul_main_add(lds, c0, lanereg, (d).x);     \
+        c1 = mul_main_add(lds, c1, lanereg, (d).y);     \
+        c2 = mul_main_add(lds, c2, lanereg, (d).z);     \
+        c3 = mul_main_add(lds, c3, lanereg, (d).w);     \
     } while (0)
     if (rem <= (uint32_t)PF) {
         chunk_prefetch<G, PF, NT>(base, nx, NW0, NA);
@@ -751,6 +924,85 @@ __device__ __forceinline__ void plan_chunks_loop(const uint32_t* lds, uint32_t l
     }
 }
 
+// Per-block work queue over the sorted chunk list (BKD_SCHED=1): block b owns positions b, b + NB,
+// b + 2NB, ... (every block the same mix of long and short chunks); its waves take rounds of one
+// chunk per group alternately from the front (longest) and the back (shortest) of that sub-list
+// through one 64-bit LDS atomic {front, back}, so short chunks (finish- and latency-bound) run
+// beside long ones (bandwidth-bound) instead of all at the end.
+template <int G, int PF, bool NT>
+__device__ __forceinline__ void plan_chunks_queue(const uint32_t* lds, uint32_t lanereg, int g,
+                                                  const uint8_t* __restrict__ base, const PlanDesc* __restrict__ descs,
+                                                  uint32_t* __restrict__ out, uint32_t* __restrict__ partials,
+                                                  unsigned long long* q) {
+    constexpr uint32_t kGPW = 64u / (uint32_t)G;  // groups per wave
+    const uint32_t NB = gridDim.x, b = blockIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int32_t gi = lane / G;
+    bool front = ((threadIdx.x >> 6) & 1u) == 0u;
+    bool exhausted = false;
+    auto fetch = [&](int32_t k) -> PlanDesc {
+        if (k < 0) return PlanDesc{0ull, 0u, 0u};
+        return descs[(uint64_t)b + (uint64_t)k * NB];
+    };
+    auto grab = [&]() -> int32_t {
+        if (exhausted) return -1;
+        unsigned long long old = 0ull;
+        const unsigned long long inc = front ? (unsigned long long)kGPW : ((unsigned long long)(0u - kGPW) << 32);
+        if (lane == 0) old = atomicAdd(q, inc);
+        const int32_t F = (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)old);
+        const int32_t B = (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)(old >> 32));
+        int32_t k;
+        if (front) k = F + gi < B ? F + gi : -1;
+        else k = B - 1 - gi >= F ? B - 1 - gi : -1;
+        if (F >= B) exhausted = true;  // wave-uniform; every later grab is empty too
+        front = !front;
+        return k;
+    };
+    auto pf_geo = [&](const ChunkGeo& nx, const ChunkGeo& cur) -> const ChunkGeo& { return nx.len ? nx : cur; };
+    auto emit = [&](const ChunkGeo& c, uint32_t v) {
+        if (g == 0 && c.len) {
+            if (c.dst & kPlanFinal) out[c.dst & ~kPlanFinal] = ~v;
+            else partials[c.dst] = v;
+        }
+    };
+    u32x4 W0x, Ax[PF], Bx[PF], W0y, Ay[PF], By[PF];
+    ChunkGeo cur = chunk_geo<G>(fetch(grab()), g);
+    PlanDesc dn = fetch(grab());
+    ChunkGeo safe = cur;
+    if (!cur.len) safe.la0 = safe.a = 0, safe.J = 1;  // hole first: prefetch base[0..16)
+    chunk_prefetch<G, PF, NT>(base, cur.len ? cur : safe, W0x, Ax);
+    for (;;) {
+        {  // current chunk in set X, prefetch into Y
+            const PlanDesc dnn = fetch(grab());
+            const ChunkGeo nx = chunk_geo<G>(dn, g);
+            const ChunkGeo& pg = pf_geo(nx, cur.len ? cur : safe);
+            const uint32_t v = cur.len ? chunk_fold<G, PF, NT>(lds, lanereg, g, base, cur, W0x, Ax, Bx, pg, W0y, Ay)
+                                       : (chunk_prefetch<G, PF, NT>(base, pg, W0y, Ay), 0u);
+            emit(cur, v);
+            if (exhausted && !__any(nx.len != 0u || (uint32_t)(dnn.s_len >> 48) != 0u)) break;
+            if (cur.len) safe = cur;
+            cur = nx;
+            dn = dnn;
+        }
+        {  // current chunk in set Y, prefetch into X
+            const PlanDesc dnn = fetch(grab());
+            const ChunkGeo nx = chunk_geo<G>(dn, g);
+            const ChunkGeo& pg = pf_geo(nx, cur.len ? cur : safe);
+            const uint32_t v = cur.len ? chunk_fold<G, PF, NT>(lds, lanereg, g, base, cur, W0y, Ay, By, pg, W0x, Ax)
+                                       : (chunk_prefetch<G, PF, NT>(base, pg, W0x, Ax), 0u);
+            emit(cur, v);
+            if (exhausted && !__any(nx.len != 0u || (uint32_t)(dnn.s_len >> 48) != 0u)) break;
+            if (cur.len) safe = cur;
+            cur = nx;
+            dn = dnn;
+        }
+    }
+}
+
+#ifndef BKD_SCHED
+#define BKD_SCHED 0
+#endif
+
 // Chunk kernel of the ragged-batch plan: one chunk per group, grid stride over the descriptor
 // list (sorted by step count, plan_kernels.hpp). Descriptors are read two rounds ahead and each
 // chunk's first loads are issued during the previous chunk (chunk_fold), X/Y register sets
@@ -762,9 +1014,18 @@ __global__ void __launch_bounds__(kBlock) crc_plan_chunks_kernel(const uint8_t* 
                                                                  const uint32_t* __restrict__ count,
                                                                  const uint32_t* __restrict__ tables,
                                                                  uint32_t* __restrict__ out,
-                                                                 uint32_t* __restrict__ partials, OvSrc ov) {
+                                                                 uint32_t* __restrict__ partials, OvSrc ov,
+                                                                 const uint32_t* __restrict__ run_flag,
+                                                                 uint32_t run_epoch) {
     using Gm = Geo<G>;
+    if (run_flag && *run_flag != run_epoch) return;  // PlanRun: only short entries this call
     __shared__ __attribute__((aligned(16))) uint32_t lds[Gm::kLdsWords];
+    __shared__ unsigned long long queue;  // {front, back} of this block's sub-list (BKD_SCHED)
+    const uint64_t n = *count;
+    const uint64_t nov = ov.count();
+    if (n == 0 && nov == 0) return;  // every entry was short or serial: no table staging
+    if (BKD_SCHED && threadIdx.x == 0)
+        queue = (unsigned long long)(n > blockIdx.x ? (n - blockIdx.x + gridDim.x - 1) / gridDim.x : 0u) << 32;
     stage_tables<G>(lds, tables);
 
     const int lane = threadIdx.x & 63;
@@ -772,9 +1033,11 @@ __global__ void __launch_bounds__(kBlock) crc_plan_chunks_kernel(const uint8_t* 
     const uint32_t lanereg = ((uint32_t)(lane & 31) << 2) | (1u << 16);
     const uint64_t ngroups = (uint64_t)gridDim.x * (kBlock / G);
     const uint64_t gid = (uint64_t)blockIdx.x * (kBlock / G) + (uint64_t)(threadIdx.x / G);
-    const uint64_t n = *count;
-    if (gid < n) plan_chunks_loop<G, PF, NT>(lds, lanereg, g, base, descs, n, gid, ngroups, out, partials);
-    const uint64_t nov = ov.count();
+    if constexpr (BKD_SCHED != 0) {
+        if (n) plan_chunks_queue<G, PF, NT>(lds, lanereg, g, base, descs, out, partials, &queue);
+    } else {
+        if (gid < n) plan_chunks_loop<G, PF, NT>(lds, lanereg, g, base, descs, n, gid, ngroups, out, partials);
+    }
     if (nov) groups_loop<G, PF, NT>(lds, lanereg, g, base, ov, nov, gid, ngroups, nullptr);
 }
 

@@ -35,6 +35,7 @@ constexpr int kMaxJC = 256;  // bins 0 .. jc + merge steps
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;  // single aligned chunk, no tail: the chunk writes out[] itself
 constexpr uint32_t kSerial = 0xFFFFFFFEu;  // whole entry folded serially by the combine kernel
 constexpr uint32_t kDirect = 0xFFFFFFFDu;  // plan capacity exceeded: serial too
+constexpr uint32_t kSmall = 0xFFFFFFFCu;   // short-entry class: computed by its own launch (SmallIndexedSrc)
 
 struct PlanGeo {
     uint32_t step;   // 16 * G bytes
@@ -45,6 +46,16 @@ struct PlanGeo {
     uint32_t nbins;  // bins 0 .. nbins-1: ceil((ch + merge - 1) / step) + 1
     uint32_t step_sh;  // log2(step)
     uint32_t ch_sh;    // log2(ch) when ch is a power of two, else 0xFF (64-bit divisions are slow)
+    uint32_t small;    // entries of <= small bytes belong to the short-entry launch (0: none do)
+};
+
+// Whether the plan has work this call: with a short-entry class, its launch (which reads every
+// length first) stores `epoch` into *flag when it meets an entry of the plan's; without, always.
+// Every plan kernel returns at once otherwise, so a batch of short entries costs them nothing.
+struct PlanRun {
+    const uint32_t* flag;
+    uint32_t epoch;
+    __device__ __forceinline__ bool on() const { return !flag || *flag == epoch; }
 };
 
 // hdr words
@@ -65,11 +76,17 @@ struct EntryPlan {
     uint32_t jh;    // head chunk steps (1 .. nbins-1)
     uint32_t full;  // chunks in the full bucket (bin JC)
     uint32_t ps;    // partial slots (0: the single chunk writes the final CRC)
-    uint32_t kind;  // 0 chunked, 1 serial, 2 invalid
+    uint32_t kind;  // 0 chunked, 1 serial, 2 invalid, 3 short-entry class (not the plan's)
 };
+
+__device__ __forceinline__ bool is_small(uint32_t l, const PlanGeo& pg) { return l <= pg.small && pg.small != 0u; }
 
 __device__ __forceinline__ EntryPlan plan_entry(uint64_t o, uint32_t l, uint64_t size, const PlanGeo& pg) {
     EntryPlan p{};
+    if (is_small(l, pg)) {  // bounds included: the short-entry launch reports them
+        p.kind = 3;
+        return p;
+    }
     if (!entry_valid(o, l, size)) {
         p.kind = 2;
         return p;
@@ -149,70 +166,81 @@ __device__ __forceinline__ uint32_t plan_ncols(const PlanGeo& pg) { return pg.nb
 __device__ __forceinline__ uint32_t slot_col(const PlanGeo& pg) { return pg.nbins; }
 
 // Per-block column counts (plan_scan_kernel turns them into per-block offsets and totals).
+// blive[b]: entries of block b that the plan itself handles (not the short-entry class); emit and
+// combine skip blocks without any (a batch of short entries costs them one word per block).
 __global__ void __launch_bounds__(kPlanBlock) plan_count_kernel(const uint64_t* __restrict__ offsets,
                                                                 const uint32_t* __restrict__ lengths, uint64_t size,
-                                                                uint64_t n, PlanGeo pg, uint32_t* __restrict__ blk) {
+                                                                uint64_t n, PlanGeo pg, uint32_t* __restrict__ blk,
+                                                                uint32_t* __restrict__ blive, uint32_t nb, PlanRun run) {
+    if (!run.on()) return;
     __shared__ uint32_t col[kMaxJC + 2];
+    __shared__ uint32_t live;
     const uint32_t ncols = plan_ncols(pg);
+    for (uint32_t eb = blockIdx.x; eb < nb; eb += gridDim.x) {  // entry blocks of 1024, grid stride
     for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) col[k] = 0u;
+    if (threadIdx.x == 0) live = 0u;
     __syncthreads();
-    const uint64_t i = (uint64_t)blockIdx.x * kPlanBlock + threadIdx.x;
-    uint32_t full = 0u, ps = 0u;
+    const uint64_t i = (uint64_t)eb * kPlanBlock + threadIdx.x;
+    uint32_t full = 0u, ps = 0u, mine = 0u;
     if (i < n) {
-        const EntryPlan p = plan_entry(offsets[i], lengths[i], size, pg);
-        if (p.kind == 0) {
-            if (p.jh != pg.jc) atomicAdd(&col[p.jh], 1u);
-            full = p.full;
-            ps = p.ps;
+        const uint32_t l = lengths[i];
+        if (!is_small(l, pg)) {  // offsets are read only for the plan's own entries
+            mine = 1u;
+            const EntryPlan p = plan_entry(offsets[i], l, size, pg);
+            if (p.kind == 0) {
+                if (p.jh != pg.jc) atomicAdd(&col[p.jh], 1u);
+                full = p.full;
+                ps = p.ps;
+            }
         }
     }
-    // every entry adds to these two columns: one LDS atomic per wave instead of 64
+    // every entry adds to these columns: one LDS atomic per wave instead of 64
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         full += (uint32_t)__shfl_xor((int)full, d);
         ps += (uint32_t)__shfl_xor((int)ps, d);
+        mine += (uint32_t)__shfl_xor((int)mine, d);
     }
     if ((threadIdx.x & 63) == 0) {
         if (full) atomicAdd(&col[pg.jc], full);
         if (ps) atomicAdd(&col[slot_col(pg)], ps);
+        if (mine) atomicAdd(&live, mine);
     }
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) blk[(uint64_t)k * gridDim.x + blockIdx.x] = col[k];
+    for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) blk[(uint64_t)k * nb + eb] = col[k];
+    if (threadIdx.x == 0) blive[eb] = live;
+    __syncthreads();  // col/live are reset for the next entry block
+    }
 }
 
-// One 64-lane block per column: exclusive scan of the column's per-block counts across blocks
-// (coalesced, 16 rows per lane in flight, carry in a register); the column total goes to
-// hdr[kHdrBase + col]. plan_emit places the bins (descending step count) from those totals.
+// One 1024-thread block per column: exclusive scan of the column's per-block counts across blocks
+// (thread t sums its run of ceil(nb / 1024) rows, one block scan of the sums, then writes its run);
+// the column total goes to hdr[kHdrBase + col]. plan_emit places the bins (descending step count)
+// from those totals. A 64-lane block per column walking the rows in order took 258 us at
+// nb = 65 536 (64 M entries) against 6 us at 1 024.
 // (Folding this scan into the count kernel's last block needs a device-scope release per block,
 // an L2 write-back on this multi-XCD part: measured 52 us instead of 7.5 + 5.8.)
-__global__ void __launch_bounds__(64) plan_scan_kernel(const uint32_t* __restrict__ blk, uint32_t nb,
-                                                       uint32_t* __restrict__ blkoff, uint32_t* __restrict__ hdr) {
+__global__ void __launch_bounds__(kPlanBlock) plan_scan_kernel(const uint32_t* __restrict__ blk, uint32_t nb,
+                                                               uint32_t* __restrict__ blkoff, uint32_t* __restrict__ hdr,
+                                                               PlanRun run) {
+    if (!run.on()) return;
+    __shared__ uint32_t wsum[kPlanBlock / 64 + 1];
     const uint32_t c = blockIdx.x;
-    const int lane = threadIdx.x;
     const uint32_t* col = blk + (uint64_t)c * nb;
     uint32_t* dst = blkoff + (uint64_t)c * nb;
-    uint32_t carry = 0;
-    for (uint32_t b1 = 0; b1 < nb; b1 += 64 * 16) {
-        uint32_t v[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const uint32_t b = b1 + (uint32_t)r * 64 + (uint32_t)lane;
-            v[r] = b < nb ? col[b] : 0u;
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const uint32_t b = b1 + (uint32_t)r * 64 + (uint32_t)lane;
-            uint32_t x = v[r];
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t y = (uint32_t)__shfl_up((int)x, d);
-                if (lane >= d) x += y;
-            }
-            if (b < nb) dst[b] = carry + x - v[r];
-            carry += (uint32_t)__shfl((int)x, 63);
-        }
+    const uint32_t per = (nb + kPlanBlock - 1u) / kPlanBlock;
+    const uint32_t b0 = threadIdx.x * per < nb ? threadIdx.x * per : nb;
+    const uint32_t b1 = b0 + per < nb ? b0 + per : nb;
+    uint32_t sum = 0u;
+    for (uint32_t b = b0; b < b1; ++b) sum += col[b];
+    uint32_t total;
+    uint32_t acc = block_excl_scan(sum, wsum, total);
+    for (uint32_t b = b0; b < b1; ++b) {
+        const uint32_t v = col[b];
+        dst[b] = acc;
+        acc += v;
     }
-    if (lane == 0) hdr[kHdrBase + c] = carry;
+    if (threadIdx.x == 0) hdr[kHdrBase + c] = total;
 }
 
 // Descriptor of chunk c of an entry from its stashed plan (plan_emit's cooperative pass).
@@ -231,45 +259,52 @@ __device__ __forceinline__ PlanDesc chunk_desc_of(int64_t ae, int64_t s0, uint32
 // Writes every chunk descriptor. Heads go to their step bin (LDS atomic cursor per bin); the full
 // chunks of the block's entries form one contiguous run in the full bin, written by the whole
 // block (one descriptor per thread per pass, coalesced, no per-entry serial loop) — including
-// entries with thousands of chunks.
+// entries with thousands of chunks. Grid stride over the nb * reps virtual blocks.
 __global__ void __launch_bounds__(kPlanBlock) plan_emit_kernel(const uint64_t* __restrict__ offsets,
                                                                const uint32_t* __restrict__ lengths,
                                                                const uint32_t* __restrict__ seeds, uint32_t seed_all,
                                                                uint64_t size, uint64_t n, PlanGeo pg,
                                                                uint64_t capacity, const uint32_t* __restrict__ blkoff,
                                                                uint32_t* __restrict__ pslot, uint32_t* __restrict__ hdr,
-                                                               PlanDesc* __restrict__ descs, uint32_t reps) {
-    // `reps` blocks per 1024-entry block (few entries, many chunks each: 256 x 16 MiB is one entry
-    // block): every replica plans the same entries, replica 0 writes heads, slots and the header,
-    // and the replicas split the block's full-chunk descriptors
-    const uint32_t eb = blockIdx.x / reps, rep = blockIdx.x - eb * reps, neb = gridDim.x / reps;
+                                                               PlanDesc* __restrict__ descs, uint32_t reps,
+                                                               const uint32_t* __restrict__ blive, uint32_t nb,
+                                                               PlanRun run) {
+    // `reps` virtual blocks per 1024-entry block (few entries, many chunks each: 256 x 16 MiB is one
+    // entry block): every replica plans the same entries, replica 0 writes heads, slots and the
+    // header, and the replicas split the block's full-chunk descriptors
+    if (!run.on()) return;
     __shared__ uint32_t wsum[kPlanBlock / 64 + 1];
+    __shared__ uint32_t bin0[kMaxJC + 2];  // first position of each bin (descending step count)
     __shared__ uint32_t cursor[kMaxJC + 2];
     __shared__ uint32_t exf[kPlanBlock + 1];  // block-exclusive scan of full-chunk counts (+ total)
     __shared__ int64_t st_ae[kPlanBlock], st_s[kPlanBlock];
     __shared__ uint32_t st_m[kPlanBlock], st_flags[kPlanBlock], st_seed[kPlanBlock], st_slot[kPlanBlock];
     __shared__ uint32_t s_total;
     const uint32_t ncols = plan_ncols(pg);
-    for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) cursor[k] = hdr[kHdrBase + k];
+    for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) bin0[k] = hdr[kHdrBase + k];
     __syncthreads();
     if (threadIdx.x == 0) {  // column totals -> first position of each bin, descending step count
         uint32_t acc = 0;
         for (int j = (int)pg.nbins - 1; j >= 0; --j) {
-            const uint32_t t = cursor[j];
-            cursor[j] = acc;
+            const uint32_t t = bin0[j];
+            bin0[j] = acc;
             acc += t;
         }
-        const uint32_t slots = cursor[slot_col(pg)];
-        cursor[slot_col(pg)] = 0;
+        const uint32_t slots = bin0[slot_col(pg)];
+        bin0[slot_col(pg)] = 0;
         s_total = acc;
-        if (blockIdx.x == 0) {  // entry block 0, replica 0
+        if (blockIdx.x == 0) {  // the block that plans entry block 0, replica 0
             hdr[kHdrTotal] = acc;
             hdr[kHdrSlots] = slots;
             hdr[kHdrWork] = (uint32_t)((uint64_t)acc < capacity ? acc : capacity);
         }
     }
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) cursor[k] += blkoff[(uint64_t)k * neb + eb];
+    const uint32_t nvb = nb * reps;
+    for (uint32_t vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
+    const uint32_t eb = vb / reps, rep = vb - eb * reps;
+    if (blive[eb] == 0u) continue;  // only short entries (block-uniform)
+    for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) cursor[k] = bin0[k] + blkoff[(uint64_t)k * nb + eb];
     __syncthreads();
     const uint64_t i = (uint64_t)eb * kPlanBlock + threadIdx.x;
     EntryPlan p{};
@@ -282,7 +317,7 @@ __global__ void __launch_bounds__(kPlanBlock) plan_emit_kernel(const uint64_t* _
     const uint32_t run0 = cursor[pg.jc];  // the block's first full-bin position (heads never move it)
     exf[threadIdx.x] = ex_full;
     if (threadIdx.x == 0) exf[kPlanBlock] = t_full;
-    if (rep == 0u && i < n && !chunked) pslot[i] = kSerial;
+    if (rep == 0u && i < n && !chunked) pslot[i] = p.kind == 3u ? kSmall : kSerial;
     if (chunked) {
         const uint32_t rs = run0 + ex_full;
         const uint32_t sb = cursor[slot_col(pg)] + ex_ps;
@@ -331,6 +366,8 @@ __global__ void __launch_bounds__(kPlanBlock) plan_emit_kernel(const uint64_t* _
             descs[pos] = chunk_desc_of(st_ae[t], st_s[t], st_m[t], fl & 0xFFu, (fl & 0x100u) != 0u, c, st_seed[t],
                                        (uint32_t)((uint64_t)eb * kPlanBlock + t), st_slot[t], pg);
         }
+    }
+    __syncthreads();  // LDS stashes and cursors are rewritten by the next virtual block
     }
 }
 
@@ -391,7 +428,7 @@ constexpr uint32_t kCombineSerial = 64;
 constexpr uint32_t kCombineWave = 4096;
 
 __device__ __forceinline__ uint32_t mul_x(const uint32_t* X, uint32_t r) {
-    return X[r & 0xffu] ^ X[256 + ((r >> 8) & 0xffu)] ^ X[512 + ((r >> 16) & 0xffu)] ^ X[768 + (r >> 24)];
+    return xor3(X[r & 0xffu], X[256 + ((r >> 8) & 0xffu)], X[512 + ((r >> 16) & 0xffu)] ^ X[768 + (r >> 24)]);
 }
 
 __global__ void __launch_bounds__(1024) plan_combine_kernel(
@@ -400,11 +437,12 @@ __global__ void __launch_bounds__(1024) plan_combine_kernel(
     const uint32_t* __restrict__ xtab, uint32_t xval, const uint32_t* __restrict__ x32tab,
     const uint32_t* __restrict__ btab, const uint32_t* __restrict__ xinv, uint32_t poly,
     const uint32_t* __restrict__ pslot, const uint32_t* __restrict__ partials, uint32_t* __restrict__ out,
-    uint32_t* __restrict__ err, uint32_t reps) {
-    // `reps` blocks per 1024-entry block (as plan_emit_kernel): each replica lists the block's
-    // entries of > kCombineSerial chunks and combines its share of them; replica 0 does the rest
-    // (invalid and serial entries are idempotent writes, cheap, and left to every replica)
-    const uint32_t eb = blockIdx.x / reps, rep = blockIdx.x - eb * reps;
+    uint32_t* __restrict__ err, uint32_t reps, const uint32_t* __restrict__ blive, uint32_t nblk, PlanRun run) {
+    // `reps` virtual blocks per 1024-entry block (as plan_emit_kernel): each replica lists the
+    // block's entries of > kCombineSerial chunks and combines its share of them; replica 0 does the
+    // rest (invalid and serial entries are idempotent writes, cheap, and left to every replica).
+    // Grid stride over the virtual blocks; the operator tables are staged once per block.
+    if (!run.on()) return;
     __shared__ uint32_t X[1024];
     __shared__ uint32_t W[1024];
     __shared__ uint32_t B[256];
@@ -415,12 +453,16 @@ __global__ void __launch_bounds__(1024) plan_combine_kernel(
     for (int k = threadIdx.x; k < 1024; k += blockDim.x) X[k] = xtab[k];
     for (int k = threadIdx.x; k < 1024; k += blockDim.x) W[k] = x32tab[k];
     for (int k = threadIdx.x; k < 256; k += blockDim.x) B[k] = btab[k];
+    const uint32_t nvb = nblk * reps;
+    for (uint32_t vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
+    const uint32_t eb = vb / reps, rep = vb - eb * reps;
+    if (blive[eb] == 0u) continue;  // only short entries: the short-entry launch wrote them
     if (threadIdx.x == 0) nbig = 0u;
     __syncthreads();
     const uint64_t i = (uint64_t)eb * blockDim.x + threadIdx.x;
     uint32_t is_big = 0u;
     const uint32_t slot = i < n ? pslot[i] : kNoSlot;
-    if (slot != kNoSlot && slot != kDirect) {
+    if (slot != kNoSlot && slot != kDirect && slot != kSmall) {
         const uint64_t o = offsets[i];
         const uint32_t l = lengths[i];
         if (!entry_valid(o, l, size)) {
@@ -512,6 +554,8 @@ __global__ void __launch_bounds__(1024) plan_combine_kernel(
             out[e] = ~reg;
         }
         __syncthreads();
+    }
+    __syncthreads();  // big[] and nbig are rebuilt by the next virtual block
     }
 }
 

@@ -249,6 +249,11 @@ BKD_API int bkd_set_plan_mode(int mode);
  * steps bytes, <= 32 KiB) and the head-merge threshold in bytes (a head chunk shorter than this
  * joins its neighbour; >= 16). Default 8, 32, 16 (4 KiB chunks; tools/tune_plan.py). */
 BKD_API int bkd_set_plan_geometry(int lanes, int steps_per_chunk, int merge_bytes);
+/* Short-entry class of indexed batches that take the plan: entries of <= max_bytes (16..192; 0 = no
+ * class) run in their own launch, 4-lane groups loading the next entry while folding the current
+ * one, and skip the plan's count/emit/chunk/combine work. Used when the base buffer
+ * holds at most 1 KiB per entry (short entries dominate). Default 192. */
+BKD_API int bkd_set_plan_small(uint32_t max_bytes);
 /* Register double-buffer depth of the plan's chunk kernel (2, 4 or 8 loads per lane). */
 BKD_API int bkd_set_plan_prefetch(int loads_in_flight);
 BKD_API int bkd_get_group_lanes(int algo, uint64_t mean_len);

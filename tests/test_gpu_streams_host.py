@@ -233,3 +233,46 @@ def test_package_batch_host_matches_oracle(gpu, algo, dtype, stride):
         assert digests[i] == d, i
         assert bytes(frames[i, :32]) == hdr
         assert bytes(frames[i, 32:32 + mac]) == oracle.digest_bytes(algo, d)
+
+
+@pytest.mark.parametrize("small", [0, 16, 100, 192])
+def test_plan_short_entry_class(gpu, small):
+    """Indexed batches through the plan with the short-entry class at several bounds: every length
+    0..700 packed at odd offsets, seeded, plus out-of-range entries on both sides of the bound — the
+    short launch and the plan together give the oracle's digests and one bounds report."""
+    import torch
+    rng = np.random.default_rng(50 + small)
+    lens = np.concatenate([np.arange(0, 701), rng.integers(0, 1000, 3000)]).astype(np.int64)
+    rng.shuffle(lens)
+    offs = np.concatenate([[3], 3 + np.cumsum(lens[:-1])]).astype(np.int64)
+    size = int(offs[-1] + lens[-1]) + 100_000  # > 256 KiB (the plan path), < 1 KiB per entry (the short class)
+    assert size > 256 << 10 and size <= 1024 * lens.size
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    seeds = rng.integers(0, 2**32, lens.size, dtype=np.uint64).astype(np.uint32)
+    want = oracle.batch(0, host, offs.astype(np.uint64), lens.astype(np.uint32), seeds=seeds)
+    base = _dev(torch, host, gpu)
+    d_seeds = _dev(torch, seeds.view(np.int32), gpu)
+    ck.set_plan_mode(2)
+    ck.set_plan_small(small)
+    try:
+        out = ck.crc_batch(0, base, _dev(torch, offs, gpu), _dev(torch, lens.astype(np.int32), gpu), seeds=d_seeds,
+                           sync_check=True)
+        assert (out.cpu().numpy().view(np.uint32) == want).all()
+        bad_o = offs.copy()
+        bad_l = lens.copy()
+        bad_o[10], bad_l[10] = size - 5, 50     # short class, out of range
+        bad_o[20], bad_l[20] = size - 5, 900    # plan class, out of range
+        with pytest.raises(BkdError) as e:
+            ck.crc_batch(0, base, _dev(torch, bad_o, gpu), _dev(torch, bad_l.astype(np.int32), gpu), seeds=d_seeds,
+                         sync_check=True)
+        assert e.value.code == -4
+        # only short entries: the plan kernels find no work of their own
+        m = (size - 1) // 37
+        sl = np.full(m, 37, dtype=np.int64)
+        so = np.arange(m, dtype=np.int64) * 37 + 1
+        out = ck.crc_batch(0, base, _dev(torch, so, gpu), _dev(torch, sl.astype(np.int32), gpu), sync_check=True)
+        want2 = oracle.batch(0, host, so.astype(np.uint64), sl.astype(np.uint32))
+        assert (out.cpu().numpy().view(np.uint32) == want2).all()
+    finally:
+        ck.set_plan_mode(0)
+        ck.set_plan_small(192)

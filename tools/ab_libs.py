@@ -34,6 +34,8 @@ def main(paths):
             if hasattr(L, fn):
                 getattr(L, fn).restype = res
                 getattr(L, fn).argtypes = args
+        if os.environ.get("AB_SMALL") and hasattr(L, "bkd_set_plan_small"):
+            L.bkd_set_plan_small(int(os.environ["AB_SMALL"]))
         libs[os.path.basename(p)] = L
     n = 1 << 20
     offs, lens = zipf_index(n)
@@ -48,11 +50,15 @@ def main(paths):
                 torch.from_numpy(np.ascontiguousarray(l).astype(np.int32)).to(dev))
 
     lt = lens < 1024
+    head_l = np.where(lens % 4096 == 0, 4096, lens % 4096)  # what the plan leaves as heads, packed alone
+    head_o = np.concatenate([[0], np.cumsum(head_l[:-1])])
     work = {
         "zipf": (0, *idx(offs, lens), total),
         "zipf_crc32": (1, *idx(offs, lens), total),
         "zipf_lt1k": (0, *idx(offs[lt], lens[lt]), int(lens[lt].sum())),
+        "zipf_heads": (0, *idx(head_o, head_l), int(head_l.sum())),
         "packed64": (0, *idx(np.arange(n) * 64, np.full(n, 64)), n * 64),
+        "packed64_64m": (0, *idx(np.arange(64 * n) * 64, np.full(64 * n, 64)), 64 * n * 64),
         "indexed4k": (0, *idx(np.arange(n) * 4096, np.full(n, 4096)), n * 4096),
     }
 

@@ -34,7 +34,7 @@ def run():
     total = int(offs[-1] + lens[-1])
     base = torch.empty(max(total, n * 4096), dtype=torch.uint8, device=dev)
     ck.fill_splitmix64(base, 42)
-    out = torch.empty(n, dtype=torch.int32, device=dev)
+    out = torch.empty(max(n, int(os.environ.get("DIAG_PACKED_N", n))), dtype=torch.int32, device=dev)
 
     def indexed(o, l):
         return torch.from_numpy(np.ascontiguousarray(o)).to(dev), torch.from_numpy(l.astype(np.int32)).to(dev)
@@ -45,12 +45,27 @@ def run():
     go, gl = indexed(offs[ge], lens[ge])
     lt = lens < 1024
     lo, ll = indexed(offs[lt], lens[lt])
+    # the Zipf entries split into what the plan makes of them: full 4 KiB chunks (lengths rounded down to
+    # 4 KiB, 4 KiB-aligned, packed: no heads) and the heads alone (len mod 4 KiB, packed, unaligned)
+    full_l = (lens // 4096) * 4096
+    fl_keep = full_l > 0
+    fo = np.zeros(int(fl_keep.sum()), dtype=np.int64)
+    np.cumsum(full_l[fl_keep][:-1], out=fo[1:])
+    fuo, ful = indexed(fo, full_l[fl_keep])
+    head_l = np.where(lens % 4096 == 0, 4096, lens % 4096)
+    ho = np.zeros(n, dtype=np.int64)
+    np.cumsum(head_l[:-1], out=ho[1:])
+    hdo, hdl = indexed(ho, head_l)
+    perm = np.random.default_rng(1).permutation(n)
+    sho, shl = indexed(np.arange(n, dtype=np.int64)[perm] * 4096, np.full(n, 4096))
+    e8o, e8l = indexed(np.arange(n // 2, dtype=np.int64) * 8192, np.full(n // 2, 8192))
 
     def plan(geom=(8, 32, 16), pf=2, algo=0, o=zo, l=zl):
         def f():
             ck.set_plan_mode(2)
             ck.set_plan_geometry(*geom)
             ck.set_plan_prefetch(pf)
+            ck.set_plan_small(int(os.environ.get("DIAG_SMALL", "0")))
             ck.crc_batch(algo, base, o, l, out=out[: o.numel()], stream=st)
         return f
 
@@ -71,6 +86,26 @@ def run():
         "zipf_lt1k_plan": plan(o=lo, l=ll),
         "zipf_lt1k_direct": direct_idx(lo, ll),
         "zipf_plan_crc32": plan(algo=1),
+        "zipf_plan_4x64": plan(geom=(4, 64, 16)),
+        "zipf_plan_4x128": plan(geom=(4, 128, 16)),
+        "zipf_plan_8x32_m4096": plan(geom=(8, 32, 4096)),
+        "zipf_plan_4x64_m4096": plan(geom=(4, 64, 4096)),
+        "zipf_plan_8x32_m1024": plan(geom=(8, 32, 1024)),
+        "zipf_plan_8x32_m512": plan(geom=(8, 32, 512)),
+        "zipf_plan_8x32_m2048": plan(geom=(8, 32, 2048)),
+        "zipf_plan_8x32_m1536": plan(geom=(8, 32, 1536)),
+        "zipf_plan_8x24_m1024": plan(geom=(8, 24, 1024)),
+        "zipf_plan_8x48_m1024": plan(geom=(8, 48, 1024)),
+        "zipf_plan_8x64_m2048": plan(geom=(8, 64, 2048)),
+        "zipf_heads_plan_4x64": plan(o=hdo, l=hdl, geom=(4, 64, 16)),
+        "zipf_lt1k_plan_4x64": plan(o=lo, l=ll, geom=(4, 64, 16)),
+        "indexed4k_shuffled_plan": plan(o=sho, l=shl),
+        "indexed4k_shuffled_direct": direct_idx(sho, shl),
+        "indexed8k_plan": plan(o=e8o, l=e8l),
+        "zipf_fullchunks_plan": plan(o=fuo, l=ful),
+        "zipf_fullchunks_direct": direct_idx(fuo, ful),
+        "zipf_heads_plan": plan(o=hdo, l=hdl),
+        "zipf_heads_direct": direct_idx(hdo, hdl),
     }
     # packed{S}_{plan|direct|plan4}: n entries of S bytes back to back (unaligned starts)
     info_pk = {}
@@ -79,7 +114,7 @@ def run():
         if not m:
             continue
         S = int(m.group(1))
-        npk = min(n, base.numel() // S)
+        npk = min(int(os.environ.get("DIAG_PACKED_N", n)), base.numel() // S)
         po, pl = indexed(np.arange(npk, dtype=np.int64) * S, np.full(npk, S))
         info_pk[name] = (npk, npk * S)
         kind = m.group(2)
@@ -87,7 +122,11 @@ def run():
                       plan(o=po, l=pl, geom=(4, 64, 16) if kind == "plan4" else (8, 32, 16)))
     info = {"zipf_ge4k_plan": (int(ge.sum()), int(lens[ge].sum())),
             "zipf_ge4k_plan_o0": (int(ge.sum()), int(lens[ge].sum())), "zipf_lt1k_plan": (int(lt.sum()), int(lens[lt].sum())),
-            "zipf_lt1k_direct": (int(lt.sum()), int(lens[lt].sum()))}
+            "zipf_lt1k_direct": (int(lt.sum()), int(lens[lt].sum())),
+            "zipf_fullchunks_plan": (int(fl_keep.sum()), int(full_l.sum())),
+            "zipf_fullchunks_direct": (int(fl_keep.sum()), int(full_l.sum())),
+            "zipf_heads_plan": (n, int(head_l.sum())), "zipf_heads_direct": (n, int(head_l.sum())),
+            "indexed8k_plan": (n // 2, n * 4096)}
     info.update(info_pk)
     ref = {}
     for name in WORKLOADS:
