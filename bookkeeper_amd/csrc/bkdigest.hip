@@ -150,7 +150,10 @@ std::atomic<int> g_plan_pf{2};  // loads in flight per lane in the chunk kernel 
 constexpr int kSmallLanes = 4;
 constexpr uint32_t kSmallMaxBytes = 16u * kSmallLanes * 3u;  // one register set per entry (PF = 2)
 std::atomic<uint32_t> g_plan_small{kSmallMaxBytes};
-constexpr uint64_t kShortClassMeanMax = 1024;  // bytes of base buffer per entry
+#ifndef BKD_SHORT_MEAN_MAX
+#define BKD_SHORT_MEAN_MAX 1024
+#endif
+constexpr uint64_t kShortClassMeanMax = BKD_SHORT_MEAN_MAX;  // bytes of base buffer per entry
 // Indexed batches whose base buffer is at most this size skip the plan (latency over balance).
 constexpr uint64_t kDirectMaxBytes = 256u << 10;
 

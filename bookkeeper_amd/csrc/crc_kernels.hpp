@@ -588,6 +588,32 @@ __device__ __forceinline__ void uniform_small_loop(const uint32_t* lds, uint32_t
     }
 }
 
+// One short-class entry of a group (kind 0 folds, 1 serial bytes, 2 bounds error, else nothing).
+template <int G, int PF>
+__device__ __forceinline__ void small_entry_finish(const uint32_t* lds, uint32_t lanereg, int g,
+                                                   const uint8_t* __restrict__ base, const SmallIndexedSrc& src,
+                                                   const SmallGeo& c, uint64_t i, const u32x4& W0,
+                                                   const u32x4 (&A)[PF], uint32_t* __restrict__ err) {
+    using Gm = Geo<G>;
+    if (c.kind == 0) {
+        const uint32_t v = small_fold<G, PF>(lds, lanereg, c, W0, A);
+        if (g == 0) src.out[i] = ~v;
+    } else if (c.kind == 1) {  // < 16 B: serial byte loop (ReflectedIntCrc.java:44-48 form)
+        if (g == 0) {
+            uint32_t r = c.r0;
+            const uint8_t* q = base + c.s;
+            for (uint32_t k = 0; k < c.len; ++k)
+                r = lds_word(lds, Gm::kByteTabOff + (((r ^ q[k]) & 0xffu) << 2)) ^ (r >> 8);
+            src.out[i] = ~r;
+        }
+    } else if (c.kind == 2) {
+        if (g == 0) {
+            src.out[i] = 0u;
+            if (err) atomicOr(err, 1u);
+        }
+    }
+}
+
 // The short-entry class of an indexed batch (SmallIndexedSrc), with uniform_small_loop's X/Y
 // lookahead: a group's next entry is loaded while the current one folds. Entries of other kinds
 // take their branch (serial bytes, bounds error, skip) without loads of their own.
@@ -597,27 +623,10 @@ __device__ __forceinline__ bool indexed_small_loop(const uint32_t* lds, uint32_t
                                                    const uint8_t* __restrict__ base, const SmallIndexedSrc& src,
                                                    uint64_t n, uint64_t gid, uint64_t ngroups,
                                                    uint32_t* __restrict__ err) {
-    using Gm = Geo<G>;
     bool saw_plan = false;
     auto finish = [&](const SmallGeo& c, uint64_t i, const u32x4& W0, const u32x4(&A)[PF]) {
         saw_plan |= c.kind == 3;
-        if (c.kind == 0) {
-            const uint32_t v = small_fold<G, PF>(lds, lanereg, c, W0, A);
-            if (g == 0) src.out[i] = ~v;
-        } else if (c.kind == 1) {  // < 16 B: serial byte loop (ReflectedIntCrc.java:44-48 form)
-            if (g == 0) {
-                uint32_t r = c.r0;
-                const uint8_t* q = base + c.s;
-                for (uint32_t k = 0; k < c.len; ++k)
-                    r = lds_word(lds, Gm::kByteTabOff + (((r ^ q[k]) & 0xffu) << 2)) ^ (r >> 8);
-                src.out[i] = ~r;
-            }
-        } else if (c.kind == 2) {
-            if (g == 0) {
-                src.out[i] = 0u;
-                if (err) atomicOr(err, 1u);
-            }
-        }
+        small_entry_finish<G, PF>(lds, lanereg, g, base, src, c, i, W0, A, err);
     };
     // index words two entries ahead, data one entry ahead (X/Y register sets)
     u32x4 W0x, Ax[PF], W0y, Ay[PF];
