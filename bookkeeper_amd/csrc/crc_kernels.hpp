@@ -230,6 +230,7 @@ __device__ __forceinline__ uint32_t lane_tree_dpp(const uint32_t* lds, uint32_t 
         return v;
     } else {
         const uint32_t other = dpp_row_shl<(1 << LV)>(v);
+        // (every lane multiplies: masking the lanes whose result is unused measured no different)
         v = mul_aux_add(lds, x32_off + 4096u * (uint32_t)(1 + LV), v, other);
         return lane_tree_dpp<LV + 1, LEVELS>(lds, x32_off, v);
     }
