@@ -850,9 +850,16 @@ int host_segments(HostStage& hs, const uint32_t* h_lengths, uint64_t n, uint64_t
 
 // ---- per-call resume (IntHash.resume) -------------------------------------------------------
 // Host buffers up to this many bytes take the CPU route (host_crc.cpp); larger ones the GPU
-// through pinned staging. Default 4 MiB: where a pageable source breaks even (one core ~210 us vs
-// ~230 us by gather + PCIe + launch, profiles/r02_call_latency.log).
-std::atomic<uint64_t> g_cpu_route_max{(uint64_t)4 << 20};
+// through pinned staging. Default from the per-call sweep (profiles/r02_call_latency.log): 4 MiB
+// with the 128-bit fold (one core ~210 us vs ~230 us by gather + PCIe + launch for a pageable
+// buffer), 64 MiB with the AVX-512 fold (one core then keeps pace with PCIe). UINT64_MAX = unset.
+std::atomic<uint64_t> g_cpu_route_max{UINT64_MAX};
+
+uint64_t cpu_route_max() {
+    const uint64_t v = g_cpu_route_max.load(std::memory_order_relaxed);
+    if (v != UINT64_MAX) return v;
+    return bkd::host::has_wide_fold() ? (64ull << 20) : (4ull << 20);
+}
 
 int cpu_resume(int algo, uint32_t current, const void* p, uint64_t len, uint32_t* out) {
     *out = ~bkd::host::crc_raw(algo, ~current, (const uint8_t*)p, (size_t)len);
@@ -1085,7 +1092,7 @@ int bkd_resume_host(int algo, uint32_t current, const void* h_ptr, uint64_t len,
         return BKD_OK;
     }
     if (!h_ptr) return fail(BKD_ERR_INVALID_ARG, "null buffer");
-    if (len <= g_cpu_route_max.load(std::memory_order_relaxed) || visible_devices() <= 0)
+    if (len <= cpu_route_max() || visible_devices() <= 0)
         return cpu_resume(algo, current, h_ptr, len, out);
     if (len > 0xFFFFFFFFull) return fail(BKD_ERR_INVALID_ARG, "len > 4 GiB - 1");
     const uint64_t off = 0;
@@ -1141,7 +1148,7 @@ int bkd_set_cpu_route_max(uint64_t bytes) {
     return BKD_OK;
 }
 
-uint64_t bkd_get_cpu_route_max(void) { return g_cpu_route_max.load(); }
+uint64_t bkd_get_cpu_route_max(void) { return cpu_route_max(); }
 
 const char* bkd_cpu_impl(void) { return bkd::host::impl_name(); }
 

@@ -14,7 +14,12 @@ namespace host {
 // resume(prev, M) = ~crc_raw(algo, ~prev, M).
 uint32_t crc_raw(int algo, uint32_t reg, const uint8_t* p, size_t n);
 
-// Which implementation crc_raw dispatches to on this CPU: "pclmul+sse4.2", "pclmul", "slice8".
+// Whether crc_raw has the AVX-512 VPCLMULQDQ path on this CPU (it then beats a GPU round trip
+// for single host buffers up to tens of MiB).
+bool has_wide_fold();
+
+// Which implementation crc_raw dispatches to on this CPU: "vpclmul512+pclmul+sse4.2", "pclmul+sse4.2",
+// "pclmul", "slice8".
 const char* impl_name();
 
 }  // namespace host

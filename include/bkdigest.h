@@ -142,10 +142,12 @@ BKD_API int bkd_resume_device(int algo, uint32_t current, const void* d_ptr, uin
                               uint32_t* out);
 BKD_API int bkd_cpu_resume(int algo, uint32_t current, const void* h_ptr, uint64_t len, uint32_t* out);
 /* Host buffers up to this many bytes take the CPU route in bkd_resume / bkd_resume_host
- * (0 = always the GPU when one is visible). Default from profiles/r02_call_latency.log. */
+ * (0 = always the GPU when one is visible). Default by CPU, from profiles/r02_call_latency.log:
+ * 64 MiB where the AVX-512 VPCLMULQDQ fold runs (a core keeps pace with PCIe), else 4 MiB. */
 BKD_API int bkd_set_cpu_route_max(uint64_t bytes);
 BKD_API uint64_t bkd_get_cpu_route_max(void);
-/* The CPU route's implementation on this host: "pclmul+sse4.2", "pclmul" or "slice8". */
+/* The CPU route's implementation on this host: "vpclmul512+pclmul+sse4.2", "pclmul+sse4.2", "pclmul"
+ * or "slice8". */
 BKD_API const char* bkd_cpu_impl(void);
 
 /* ---- circe-checksum compatibility (the Sse42Crc32C natives, $CN/cpp/crc32c_sse42_jni.cpp) -----

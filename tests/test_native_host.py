@@ -76,13 +76,13 @@ def test_cpu_route_against_golden_and_oracle(algo):
         assert got == int(fx[key][i], 16), i
     rng = np.random.default_rng(77 + algo)
     buf = rng.integers(0, 256, 1 << 17, dtype=np.uint8)
-    lengths = list(range(0, 601)) + [1023, 1024, 1025, 4095, 4096, 4097, 65535, 65536, 100000]
+    lengths = list(range(0, 601)) + [1023, 1024, 1025, 1279, 1280, 1281, 4095, 4096, 4097, 65535, 65536, 100000]
     for n in lengths:
         off = int(rng.integers(0, 64))
         seed = int(rng.integers(0, 2**32))
         want = oracle.resume(algo, seed, buf[off:off + n])
         assert ck.cpu_resume(algo, seed, buf[off:off + n]) & 0xFFFFFFFF == want, n
-    assert ck.cpu_impl() in ("pclmul+sse4.2", "pclmul", "slice8")
+    assert ck.cpu_impl() in ("vpclmul512+pclmul+sse4.2", "pclmul+sse4.2", "pclmul", "slice8")
 
 
 def test_cpu_route_threshold_setting():
