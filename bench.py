@@ -142,17 +142,17 @@ def cpu_baseline(host_sample: np.ndarray, entry_len: int, algo: int = 0, budget_
         kind = "reference"
         run = lambda thr, reps: ref.ref_crc32c_uniform_timed(u8p, entry_len, entry_len, n, thr, reps, o32)
         label = "circe crc32c() (crc32c_sse42.cpp, chunk ladder {4096,512,64}) compiled from /root/reference"
-    else:  # the C restatement (byte-table loop), single pass per rep
+    else:  # CRC-32: the JDK intrinsic's PCLMULQDQ folding, restated (oracle/cpu_baseline.c)
         kind = "port"
         lib = oracle.lib()
+        offs = np.arange(n, dtype=np.uint64) * np.uint64(entry_len)
+        lens = np.full(n, entry_len, dtype=np.uint32)
 
         def run(thr, reps):
-            t0 = time.perf_counter()
-            for _ in range(reps):
-                lib.oracle_uniform(algo, u8p, entry_len, entry_len, n, 0, o32)
-            return time.perf_counter() - t0
-        cores = 1
-        label = "oracle/crc_oracle.c byte-table restatement"
+            return lib.oracle_pclmul_crc32_batch_timed(u8p, offs.ctypes.data_as(oracle._u64p),
+                                                       lens.ctypes.data_as(oracle._u32p), n, thr, reps, o32)
+        label = ("PCLMULQDQ 4x128-bit folding (the arithmetic of java.util.zip.CRC32's HotSpot intrinsic), "
+                 "oracle/cpu_baseline.c")
     t1 = run(1, 1)  # calibrate on one core
     one_core = host_sample.size / t1 / GIB
     reps = max(1, int(budget_s / max(1e-6, t1 / cores)))
@@ -167,8 +167,8 @@ def cpu_baseline(host_sample: np.ndarray, entry_len: int, algo: int = 0, budget_
 
 def cpu_baseline_indexed(host: np.ndarray, offs: np.ndarray, lens: np.ndarray, algo: int = 0, budget_s: float = 8.0):
     """Config 3's CPU leg: one CRC per entry of an offset+length sample on the host cores. CRC32C:
-    the reference's own circe crc32c() (oracle/_ref); CRC32: zlib's crc32(), the arithmetic
-    java.util.zip.CRC32 runs (CRC32DigestManager.java:28-87)."""
+    the reference's own circe crc32c() (oracle/_ref); CRC32: the PCLMULQDQ folding java.util.zip.CRC32's
+    intrinsic runs (CRC32DigestManager.java:28-87), restated in oracle/cpu_baseline.c."""
     import oracle
     cores, cores_why = host_cores()
     n = offs.size
@@ -185,15 +185,15 @@ def cpu_baseline_indexed(host: np.ndarray, offs: np.ndarray, lens: np.ndarray, a
                                               n, thr, reps, out.ctypes.data_as(oracle._u32p))
     else:
         kind = "port"
-        label = ("zlib crc32() (the arithmetic of java.util.zip.CRC32, whose JDK intrinsic is PCLMUL-based and "
-                 "faster than this zlib 1.2.11 table loop), oracle/cpu_baseline.c")
+        label = ("PCLMULQDQ 4x128-bit folding, the arithmetic of java.util.zip.CRC32's HotSpot intrinsic "
+                 "(CRC32DigestManager.java:28-87), oracle/cpu_baseline.c")
         lib = oracle.lib()
         u8p = host.ctypes.data_as(oracle._u8p)
 
         def run(thr, reps):
-            return lib.oracle_zlib_crc32_batch_timed(u8p, o64.ctypes.data_as(oracle._u64p),
-                                                     l32.ctypes.data_as(oracle._u32p), n, thr, reps,
-                                                     out.ctypes.data_as(oracle._u32p))
+            return lib.oracle_pclmul_crc32_batch_timed(u8p, o64.ctypes.data_as(oracle._u64p),
+                                                       l32.ctypes.data_as(oracle._u32p), n, thr, reps,
+                                                       out.ctypes.data_as(oracle._u32p))
     nbytes = int(l32.sum())
     t1 = run(1, 1)
     reps = max(1, int(budget_s / max(1e-6, t1 / cores)))

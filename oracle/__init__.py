@@ -90,6 +90,9 @@ def lib():
         L.oracle_zlib_crc32_batch_timed.restype = ctypes.c_double
         L.oracle_zlib_crc32_batch_timed.argtypes = [_u8p, _u64p, _u32p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
                                                     _u32p]
+        L.oracle_pclmul_crc32_batch_timed.restype = ctypes.c_double
+        L.oracle_pclmul_crc32_batch_timed.argtypes = [_u8p, _u64p, _u32p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                                      _u32p]
         L.oracle_table.restype = None
         L.oracle_table.argtypes = [ctypes.c_int, _u32p]
         _lib = L

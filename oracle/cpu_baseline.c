@@ -57,3 +57,100 @@ double oracle_zlib_crc32_batch_timed(const uint8_t* base, const uint64_t* offs, 
     clock_gettime(CLOCK_MONOTONIC, &t1);
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
+
+/*
+ * CPU baseline for CRC-32 closer to what the JVM runs: java.util.zip.CRC32's HotSpot intrinsic on
+ * x86-64 folds 128-bit blocks with PCLMULQDQ (four accumulators, 64-byte stride) instead of zlib's
+ * table loop. Restated here with the same folding arithmetic — four accumulators of 16 bytes move
+ * 512 bits forward as clmul(lo, x^(63+512)) ^ clmul(hi, x^(512-1)) mod P (reflected operands), are
+ * merged, and the 16-byte remainder and the tail bytes are finished by zlib's crc32(). Used only for
+ * the timed baseline; its digests are checked against the GPU's in bench.py.
+ */
+#include <immintrin.h>
+#include <string.h>
+
+static uint32_t xpow_bits(uint64_t e) { /* x^e mod P, CRC-32 reflected (bit 31 = x^0) */
+    uint32_t r = 0x80000000u;
+    while (e--) r = (r >> 1) ^ ((r & 1u) ? 0xEDB88320u : 0u);
+    return r;
+}
+
+static uint64_t kq[2][2]; /* {x^(63+D), x^(D-1)} << 32 for D = 512 and D = 128 */
+static int kq_ready = 0;
+
+__attribute__((target("pclmul,sse4.2"))) static __m128i fold128(__m128i x, const uint64_t* k) {
+    const __m128i kk = _mm_set_epi64x((long long)k[1], (long long)k[0]);
+    return _mm_xor_si128(_mm_clmulepi64_si128(x, kk, 0x00), _mm_clmulepi64_si128(x, kk, 0x11));
+}
+
+__attribute__((target("pclmul,sse4.2"))) static uint32_t crc32_pclmul(const uint8_t* p, uint64_t n) {
+    if (n < 64) return (uint32_t)crc32(0L, p, (uInt)n);
+    __m128i x0 = _mm_loadu_si128((const __m128i*)p), x1 = _mm_loadu_si128((const __m128i*)(p + 16)),
+            x2 = _mm_loadu_si128((const __m128i*)(p + 32)), x3 = _mm_loadu_si128((const __m128i*)(p + 48));
+    x0 = _mm_xor_si128(x0, _mm_cvtsi32_si128((int)0xFFFFFFFF)); /* init ~0 into the first 4 bytes */
+    p += 64;
+    n -= 64;
+    while (n >= 64) {
+        x0 = _mm_xor_si128(fold128(x0, kq[0]), _mm_loadu_si128((const __m128i*)p));
+        x1 = _mm_xor_si128(fold128(x1, kq[0]), _mm_loadu_si128((const __m128i*)(p + 16)));
+        x2 = _mm_xor_si128(fold128(x2, kq[0]), _mm_loadu_si128((const __m128i*)(p + 32)));
+        x3 = _mm_xor_si128(fold128(x3, kq[0]), _mm_loadu_si128((const __m128i*)(p + 48)));
+        p += 64;
+        n -= 64;
+    }
+    __m128i x = _mm_xor_si128(fold128(x0, kq[1]), x1);
+    x = _mm_xor_si128(fold128(x, kq[1]), x2);
+    x = _mm_xor_si128(fold128(x, kq[1]), x3);
+    while (n >= 16) {
+        x = _mm_xor_si128(fold128(x, kq[1]), _mm_loadu_si128((const __m128i*)p));
+        p += 16;
+        n -= 16;
+    }
+    uint8_t b[16];
+    _mm_storeu_si128((__m128i*)b, x);
+    /* raw register of the remainder from zero = ~crc32(~0 ...), then the tail bytes */
+    uint32_t raw = ~(uint32_t)crc32(0xFFFFFFFFuL, b, 16);
+    return (uint32_t)crc32((uLong)~raw, p, (uInt)n);
+}
+
+static void* prun(void* q) {
+    zjob* j = (zjob*)q;
+    for (uint64_t i = j->lo; i < j->hi; ++i) j->out[i] = crc32_pclmul(j->base + j->offs[i], j->lens[i]);
+    return NULL;
+}
+
+double oracle_pclmul_crc32_batch_timed(const uint8_t* base, const uint64_t* offs, const uint32_t* lens, uint64_t n,
+                                       int threads, int reps, uint32_t* out) {
+    if (!kq_ready) {
+        kq[0][0] = (uint64_t)xpow_bits(63 + 512) << 32;
+        kq[0][1] = (uint64_t)xpow_bits(512 - 1) << 32;
+        kq[1][0] = (uint64_t)xpow_bits(63 + 128) << 32;
+        kq[1][1] = (uint64_t)xpow_bits(128 - 1) << 32;
+        kq_ready = 1;
+    }
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    uint64_t cut[257];
+    uint64_t total = 0, acc = 0;
+    for (uint64_t i = 0; i < n; ++i) total += lens[i];
+    cut[0] = 0;
+    for (int t = 1; t <= threads; ++t) cut[t] = n;
+    int t = 1;
+    for (uint64_t i = 0; i < n && t < threads; ++i) {
+        acc += lens[i];
+        while (t < threads && acc * (uint64_t)threads >= total * (uint64_t)t) cut[t++] = i + 1;
+    }
+    pthread_t th[256];
+    zjob jobs[256];
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int r = 0; r < reps; ++r) {
+        for (int k = 0; k < threads; ++k) {
+            jobs[k] = (zjob){base, offs, lens, cut[k], cut[k + 1], out};
+            pthread_create(&th[k], NULL, prun, &jobs[k]);
+        }
+        for (int k = 0; k < threads; ++k) pthread_join(th[k], NULL);
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
