@@ -68,6 +68,7 @@ struct StreamScratch {
     uint32_t* h_err = nullptr;
     // PlanRun word of the plans enqueued on this stream and the epoch of the latest one
     uint32_t* run = nullptr;
+    uint32_t* uni = nullptr;  // PlanRun uniform-lengths word (the epoch of the call it holds for)
     uint32_t epoch = 0;
     hipError_t run_word(hipStream_t st, uint32_t** out) {
         if (!run) {
@@ -79,6 +80,18 @@ struct StreamScratch {
             }
         }
         *out = run;
+        return hipSuccess;
+    }
+    hipError_t uni_word(hipStream_t st, uint32_t** out) {
+        if (!uni) {
+            hipError_t e = hipMallocAsync((void**)&uni, sizeof(uint32_t), st);
+            if (e == hipSuccess) e = hipMemsetAsync(uni, 0, sizeof(uint32_t), st);
+            if (e != hipSuccess) {
+                uni = nullptr;
+                return e;
+            }
+        }
+        *out = uni;
         return hipSuccess;
     }
     hipError_t flag(hipStream_t st, uint32_t** out) {
@@ -324,26 +337,27 @@ int dispatch_lanes(DeviceState& ds, int lanes, int algo, const uint8_t* base, co
 }
 
 template <int G>
-void launch_plan_chunks(const uint32_t* run_flag, uint32_t run_epoch, const uint8_t* base, const bkd::PlanDesc* descs,
+void launch_plan_chunks(const bkd::PlanRun& run, const uint8_t* base, const bkd::PlanDesc* descs,
                         const uint32_t* count, const uint32_t* tab,
-                        uint32_t* out, uint32_t* partials, const bkd::PlanDirectSrc& ov, int blocks, hipStream_t st) {
+                        uint32_t* out, uint32_t* partials, const bkd::PlanDirectSrc& ov, int blocks, hipStream_t st,
+                        uint32_t* err) {
     const int pf = g_plan_pf.load();
     if (pf == 8)
         hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 8, kNT, bkd::PlanDirectSrc>), dim3((unsigned)blocks),
-                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run_flag, run_epoch);
+                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err);
     else if (pf == 4)
         hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 4, kNT, bkd::PlanDirectSrc>), dim3((unsigned)blocks),
-                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run_flag, run_epoch);
+                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err);
     else
         hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 2, kNT, bkd::PlanDirectSrc>), dim3((unsigned)blocks),
-                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run_flag, run_epoch);
+                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err);
 }
 
 // Indexed batch through the chunked plan (plan_kernels.hpp): five stream-ordered kernels, no
 // host sync, scratch from the stream's arena.
 int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, const uint64_t* offsets,
                 const uint32_t* lengths, uint64_t n, const uint32_t* seeds, uint32_t seed_all, uint32_t* out,
-                hipStream_t st, bool short_class = true) {
+                hipStream_t st, bool short_class = true, bool direct_gate = true) {
     if (n == 0) return BKD_OK;
     if (n >= 0xFFFFFFF0ull) return fail(BKD_ERR_INVALID_ARG, "indexed batches hold fewer than 2^32 - 16 entries");
     const int G = g_plan_lanes.load();
@@ -370,6 +384,7 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     const uint32_t ncols = pg.nbins + 1u;
     Carver cv;
     const size_t o_blk = cv.take((size_t)nb * ncols * 4), o_live = cv.take((size_t)nb * 4),
+                 o_bok = cv.take((size_t)nb * 4),
                  o_blkoff = cv.take((size_t)nb * ncols * 4), o_hdr = cv.take(bkd::kHdrWords * 4),
                  o_ps = cv.take((size_t)n * 4), o_part = cv.take((size_t)capacity * 4),
                  o_desc = cv.take((size_t)capacity * sizeof(bkd::PlanDesc));
@@ -378,17 +393,24 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     uint8_t* sb = nullptr;
     uint32_t* err = nullptr;
     uint32_t* run_word = nullptr;
+    uint32_t* uni = nullptr;
+    // without a short class (mean entry > 1 KiB), lengths within an eighth of each other skip the
+    // chunks: the chunk kernel computes them whole, as the direct kernel would (PlanRun::uniform,
+    // decided on the device: plan_count's per-block ballots, reduced by plan_scan). Only where the
+    // direct kernel would use the plan's lane count.
+#ifndef BKD_DIRECT_GATE
+#define BKD_DIRECT_GATE 1
+#endif
+    const bool gate = BKD_DIRECT_GATE && pg.small == 0u && direct_gate && auto_lanes(size / n, n, ds.cus) == G;
     hipError_t e = sc.get(0, cv.used, st, &sb);
     if (e == hipSuccess) e = sc.flag(st, &err);
     if (e == hipSuccess && pg.small) e = sc.run_word(st, &run_word);
+    if (e == hipSuccess && gate) e = sc.uni_word(st, &uni);
     if (e != hipSuccess) return fail(BKD_ERR_NOMEM, std::string("plan scratch: ") + hipGetErrorString(e));
-    // with a short-entry class the plan kernels run only if that launch met one of their entries
-    bkd::PlanRun run{nullptr, 0u};
-    if (pg.small) {
-        if (++sc.epoch == 0u) ++sc.epoch;  // 0 is the word's initial value
-        run = bkd::PlanRun{run_word, sc.epoch};
-    }
+    if (++sc.epoch == 0u) ++sc.epoch;  // 0 is the words' initial value
+    const bkd::PlanRun run{run_word, uni, sc.epoch};
     uint32_t *blk = Carver::at<uint32_t>(sb, o_blk), *blive = Carver::at<uint32_t>(sb, o_live),
+             *bok = gate ? Carver::at<uint32_t>(sb, o_bok) : nullptr,
              *blkoff = Carver::at<uint32_t>(sb, o_blkoff), *hdr = Carver::at<uint32_t>(sb, o_hdr),
              *pslot = Carver::at<uint32_t>(sb, o_ps), *partials = Carver::at<uint32_t>(sb, o_part);
     bkd::PlanDesc* descs = Carver::at<bkd::PlanDesc>(sb, o_desc);
@@ -406,20 +428,21 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
 #endif
     const uint32_t pgrid = BKD_PLAN_GRID ? (uint32_t)BKD_PLAN_GRID * (uint32_t)ds.cus : 0xFFFFFFFFu;
     hipLaunchKernelGGL(bkd::plan_count_kernel, dim3(std::min(nb, pgrid)), dim3(bkd::kPlanBlock), 0, st, offsets,
-                       lengths, size, n, pg, blk, blive, nb, run);
-    hipLaunchKernelGGL(bkd::plan_scan_kernel, dim3(ncols), dim3(bkd::kPlanBlock), 0, st, blk, nb, blkoff, hdr, run);
+                       lengths, size, n, pg, blk, blive, nb, run, bok);
+    hipLaunchKernelGGL(bkd::plan_scan_kernel, dim3(ncols + (gate ? 1u : 0u)), dim3(bkd::kPlanBlock), 0, st, blk, nb,
+                       blkoff, hdr, run, ncols, bok);
     // few entry blocks (large entries): replicate emit and combine blocks so ~2 blocks per CU work
     const uint32_t reps = nb >= 2u * (uint32_t)ds.cus ? 1u : std::min<uint32_t>(64u, (2u * (uint32_t)ds.cus + nb - 1u) / nb);
     hipLaunchKernelGGL(bkd::plan_emit_kernel, dim3(std::min(nb * reps, pgrid)), dim3(bkd::kPlanBlock), 0, st, offsets,
                        lengths, seeds, seed_all, size, n, pg, capacity, blkoff, pslot, hdr, descs, reps, blive, nb, run);
     const uint32_t* tab = ds.tables[algo][lane_index(G)];
-    const bkd::PlanDirectSrc ov{n, offsets, lengths, seeds, seed_all, size, out, pslot, hdr, capacity};
+    const bkd::PlanDirectSrc ov{n, offsets, lengths, seeds, seed_all, size, out, pslot, hdr, capacity, false};
     switch (G) {
-        case 4: launch_plan_chunks<4>(run.flag, run.epoch, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st); break;
-        case 8: launch_plan_chunks<8>(run.flag, run.epoch, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st); break;
-        case 16: launch_plan_chunks<16>(run.flag, run.epoch, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st); break;
-        case 32: launch_plan_chunks<32>(run.flag, run.epoch, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st); break;
-        default: launch_plan_chunks<64>(run.flag, run.epoch, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st); break;
+        case 4: launch_plan_chunks<4>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err); break;
+        case 8: launch_plan_chunks<8>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err); break;
+        case 16: launch_plan_chunks<16>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err); break;
+        case 32: launch_plan_chunks<32>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err); break;
+        default: launch_plan_chunks<64>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err); break;
     }
     const uint32_t* btab = tab + bkd::gf2::byte_table_offset(G);
     hipLaunchKernelGGL(bkd::plan_combine_kernel, dim3(std::min(nb * reps, pgrid)), dim3(1024), 0, st, base, offsets, lengths, seeds,
@@ -921,7 +944,7 @@ int resume_device(int algo, uint32_t current, const void* ptr, uint64_t len, hip
         c->h_out[1] = l32;
         const hipError_t e = hipMemcpyAsync(c->d_len, c->h_out + 1, 4, hipMemcpyHostToDevice, st);
         rc = e == hipSuccess ? launch_plan(*ds, algo, (const uint8_t*)ptr, len, c->d_off, c->d_len, 1, nullptr,
-                                           current, c->d_out, st, false)
+                                           current, c->d_out, st, false, false)
                              : fail(BKD_ERR_HIP, hipGetErrorString(e));
     }
     if (!rc) {

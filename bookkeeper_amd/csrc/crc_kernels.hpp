@@ -215,6 +215,30 @@ struct SmallIndexedSrc {
     __device__ __forceinline__ uint64_t count() const { return n; }
 };
 
+// Which launches of an indexed call through the plan have work (no host sync decides it):
+//  * with a short-entry class, its launch (which reads every length first) stores `epoch` into
+//    *flag when it meets an entry of the plan's; without one, the plan always has entries;
+//  * with a uniformity gate, plan_count ballots each entry block's lengths against the first
+//    entry's (in_band) and plan_scan's extra block stores `epoch` into *uni when every block
+//    agreed (no reset between calls). Lengths that close are balanced one entry per lane group
+//    already: emit and combine return at once and the chunk kernel computes every entry whole,
+//    as the direct kernel does (PlanDirectSrc::all) — no extra launch. The choice only picks the
+//    schedule; both give the same digests.
+struct PlanRun {
+    const uint32_t* flag;
+    const uint32_t* uni;
+    uint32_t epoch;
+    __device__ __forceinline__ bool plan_entries() const { return !flag || *flag == epoch; }
+    __device__ __forceinline__ bool uniform() const { return uni && *uni == epoch; }
+    __device__ __forceinline__ bool on() const { return plan_entries() && !uniform(); }
+    // (emit, chunk and combine test on(); plan_count and plan_scan run before it is known)
+    // within 1/16 of the reference length + half a 128-byte line either way
+    __device__ static __forceinline__ bool in_band(uint32_t l, uint32_t ref) {
+        const uint32_t d = l > ref ? l - ref : ref - l;
+        return d <= ref / 16u + 64u;
+    }
+};
+
 // DPP row_shl:SH — lane i receives lane i + SH of its 16-lane row (0 past the row end).
 template <int SH>
 __device__ __forceinline__ uint32_t dpp_row_shl(uint32_t v) {
@@ -1025,13 +1049,14 @@ __global__ void __launch_bounds__(kBlock) crc_plan_chunks_kernel(const uint8_t* 
                                                                  const uint32_t* __restrict__ tables,
                                                                  uint32_t* __restrict__ out,
                                                                  uint32_t* __restrict__ partials, OvSrc ov,
-                                                                 const uint32_t* __restrict__ run_flag,
-                                                                 uint32_t run_epoch) {
+                                                                 PlanRun run, uint32_t* __restrict__ err) {
     using Gm = Geo<G>;
-    if (run_flag && *run_flag != run_epoch) return;  // PlanRun: only short entries this call
+    if (!run.plan_entries()) return;  // only short entries
     __shared__ __attribute__((aligned(16))) uint32_t lds[Gm::kLdsWords];
     __shared__ unsigned long long queue;  // {front, back} of this block's sub-list (BKD_SCHED)
-    const uint64_t n = *count;
+    // lengths within an eighth of each other: no chunks, every entry whole as in the direct kernel
+    ov.all = run.uniform();
+    const uint64_t n = ov.all ? 0u : *count;
     const uint64_t nov = ov.count();
     if (n == 0 && nov == 0) return;  // every entry was short or serial: no table staging
     if (BKD_SCHED && threadIdx.x == 0)
@@ -1048,7 +1073,7 @@ __global__ void __launch_bounds__(kBlock) crc_plan_chunks_kernel(const uint8_t* 
     } else {
         if (gid < n) plan_chunks_loop<G, PF, NT>(lds, lanereg, g, base, descs, n, gid, ngroups, out, partials);
     }
-    if (nov) groups_loop<G, PF, NT>(lds, lanereg, g, base, ov, nov, gid, ngroups, nullptr);
+    if (nov) groups_loop<G, PF, NT>(lds, lanereg, g, base, ov, nov, gid, ngroups, err);
 }
 
 // ---- synthetic input: little-endian splitmix64 stream ----

@@ -49,15 +49,6 @@ struct PlanGeo {
     uint32_t small;    // entries of <= small bytes belong to the short-entry launch (0: none do)
 };
 
-// Whether the plan has work this call: with a short-entry class, its launch (which reads every
-// length first) stores `epoch` into *flag when it meets an entry of the plan's; without, always.
-// Every plan kernel returns at once otherwise, so a batch of short entries costs them nothing.
-struct PlanRun {
-    const uint32_t* flag;
-    uint32_t epoch;
-    __device__ __forceinline__ bool on() const { return !flag || *flag == epoch; }
-};
-
 // hdr words
 constexpr int kHdrTotal = 0;  // all chunks
 constexpr int kHdrSlots = 1;  // partial slots
@@ -171,19 +162,26 @@ __device__ __forceinline__ uint32_t slot_col(const PlanGeo& pg) { return pg.nbin
 __global__ void __launch_bounds__(kPlanBlock) plan_count_kernel(const uint64_t* __restrict__ offsets,
                                                                 const uint32_t* __restrict__ lengths, uint64_t size,
                                                                 uint64_t n, PlanGeo pg, uint32_t* __restrict__ blk,
-                                                                uint32_t* __restrict__ blive, uint32_t nb, PlanRun run) {
-    if (!run.on()) return;
+                                                                uint32_t* __restrict__ blive, uint32_t nb, PlanRun run,
+                                                                uint32_t* __restrict__ bok) {
+    if (!run.plan_entries()) return;
     __shared__ uint32_t col[kMaxJC + 2];
-    __shared__ uint32_t live;
+    __shared__ uint32_t live, bad;
     const uint32_t ncols = plan_ncols(pg);
+    const uint32_t ref = bok ? lengths[0] : 0u;  // the uniformity ballot's reference length
     for (uint32_t eb = blockIdx.x; eb < nb; eb += gridDim.x) {  // entry blocks of 1024, grid stride
     for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) col[k] = 0u;
-    if (threadIdx.x == 0) live = 0u;
+    if (threadIdx.x == 0) {
+        live = 0u;
+        bad = 0u;
+    }
     __syncthreads();
     const uint64_t i = (uint64_t)eb * kPlanBlock + threadIdx.x;
     uint32_t full = 0u, ps = 0u, mine = 0u;
+    bool ok = true;  // length within the band of the reference (PlanRun::in_band)
     if (i < n) {
         const uint32_t l = lengths[i];
+        ok = PlanRun::in_band(l, ref);
         if (!is_small(l, pg)) {  // offsets are read only for the plan's own entries
             mine = 1u;
             const EntryPlan p = plan_entry(offsets[i], l, size, pg);
@@ -201,14 +199,19 @@ __global__ void __launch_bounds__(kPlanBlock) plan_count_kernel(const uint64_t* 
         ps += (uint32_t)__shfl_xor((int)ps, d);
         mine += (uint32_t)__shfl_xor((int)mine, d);
     }
+    const bool wave_ok = __all(ok);
     if ((threadIdx.x & 63) == 0) {
         if (full) atomicAdd(&col[pg.jc], full);
         if (ps) atomicAdd(&col[slot_col(pg)], ps);
         if (mine) atomicAdd(&live, mine);
+        if (!wave_ok) bad = 1u;  // (a per-wave min/max with global atomics cost +330 us per 1 M entries)
     }
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) blk[(uint64_t)k * nb + eb] = col[k];
-    if (threadIdx.x == 0) blive[eb] = live;
+    if (threadIdx.x == 0) {
+        blive[eb] = live;
+        if (bok) bok[eb] = bad ^ 1u;
+    }
     __syncthreads();  // col/live are reset for the next entry block
     }
 }
@@ -222,10 +225,18 @@ __global__ void __launch_bounds__(kPlanBlock) plan_count_kernel(const uint64_t* 
 // an L2 write-back on this multi-XCD part: measured 52 us instead of 7.5 + 5.8.)
 __global__ void __launch_bounds__(kPlanBlock) plan_scan_kernel(const uint32_t* __restrict__ blk, uint32_t nb,
                                                                uint32_t* __restrict__ blkoff, uint32_t* __restrict__ hdr,
-                                                               PlanRun run) {
-    if (!run.on()) return;
+                                                               PlanRun run, uint32_t ncols,
+                                                               const uint32_t* __restrict__ bok) {
+    if (!run.plan_entries()) return;
     __shared__ uint32_t wsum[kPlanBlock / 64 + 1];
     const uint32_t c = blockIdx.x;
+    if (c == ncols) {  // the extra block: PlanRun::uniform for the whole batch
+        uint32_t ok = 1u;
+        for (uint32_t b = threadIdx.x; b < nb; b += kPlanBlock) ok &= bok[b];
+        ok = (uint32_t)__syncthreads_and((int)ok);
+        if (threadIdx.x == 0) *const_cast<uint32_t*>(run.uni) = ok ? run.epoch : 0u;
+        return;
+    }
     const uint32_t* col = blk + (uint64_t)c * nb;
     uint32_t* dst = blkoff + (uint64_t)c * nb;
     const uint32_t per = (nb + kPlanBlock - 1u) / kPlanBlock;
@@ -384,12 +395,16 @@ struct PlanDirectSrc {
     const uint32_t* pslot;
     const uint32_t* hdr;
     uint64_t capacity;
-    __device__ __forceinline__ uint64_t count() const { return (uint64_t)hdr[kHdrTotal] > capacity ? n : 0u; }
+    bool all;  // set by the chunk kernel: PlanRun::uniform, every entry is computed here
+    __device__ __forceinline__ uint64_t count() const {
+        return all || (uint64_t)hdr[kHdrTotal] > capacity ? n : 0u;
+    }
     __device__ __forceinline__ int get(uint64_t i, Work& w) const {
-        if (pslot[i] != kDirect) return 3;
+        if (!all && pslot[i] != kDirect) return 3;
         w.dst = out + i;
         w.s = (int64_t)offsets[i];
         w.len = lengths[i];
+        if (!entry_valid((uint64_t)w.s, w.len, size)) return 2;
         w.r0 = ~(seeds ? seeds[i] : seed_all);
         w.xorout = 0xFFFFFFFFu;
         return 0;

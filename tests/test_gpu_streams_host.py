@@ -276,3 +276,35 @@ def test_plan_short_entry_class(gpu, small):
     finally:
         ck.set_plan_mode(0)
         ck.set_plan_small(192)
+
+
+@pytest.mark.parametrize("lo,hi", [(3600, 4096), (4096, 4096), (3000, 4096), (1200, 1300)])
+def test_plan_near_uniform_lengths(gpu, lo, hi):
+    """Plan-path batches whose lengths all lie within 1/16 (+ 64 B) of the first entry's skip the
+    chunks: the chunk kernel computes each entry whole (PlanRun::uniform). Both sides of that band
+    give the oracle's digests, seeded, and an out-of-range entry is still reported."""
+    import torch
+    rng = np.random.default_rng(lo + hi)
+    n = 6000
+    lens = rng.integers(lo, hi + 1, n).astype(np.int64)
+    offs = np.concatenate([[5], 5 + np.cumsum(lens[:-1] + 3)]).astype(np.int64)
+    size = int(offs[-1] + lens[-1]) + 777
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    base = _dev(torch, host, gpu)
+    d_seeds = _dev(torch, seeds.view(np.int32), gpu)
+    ck.set_plan_mode(2)
+    try:
+        for algo in (0, 1):
+            want = oracle.batch(algo, host, offs.astype(np.uint64), lens.astype(np.uint32), seeds=seeds)
+            out = ck.crc_batch(algo, base, _dev(torch, offs, gpu), _dev(torch, lens.astype(np.int32), gpu),
+                               seeds=d_seeds, sync_check=True)
+            assert (out.cpu().numpy().view(np.uint32) == want).all(), algo
+        bad_o = offs.copy()
+        bad_o[n // 2] = size - 100
+        with pytest.raises(BkdError) as e:
+            ck.crc_batch(0, base, _dev(torch, bad_o, gpu), _dev(torch, lens.astype(np.int32), gpu), seeds=d_seeds,
+                         sync_check=True)
+        assert e.value.code == -4
+    finally:
+        ck.set_plan_mode(0)
