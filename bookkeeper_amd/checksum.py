@@ -316,6 +316,11 @@ def set_plan_small(max_bytes: int = 192) -> None:
     check(lib().bkd_set_plan_small(max_bytes))
 
 
+def set_plan_serial(max_bytes: int = 16) -> None:
+    """Plan entries shorter than max_bytes (16..256) are computed by the combine kernel, one thread each."""
+    check(lib().bkd_set_plan_serial(max_bytes))
+
+
 def set_plan_prefetch(loads_in_flight: int = 2) -> None:
     check(lib().bkd_set_plan_prefetch(loads_in_flight))
 

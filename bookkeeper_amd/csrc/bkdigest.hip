@@ -163,6 +163,13 @@ std::atomic<int> g_plan_pf{2};  // loads in flight per lane in the chunk kernel 
 constexpr int kSmallLanes = 4;
 constexpr uint32_t kSmallMaxBytes = 16u * kSmallLanes * 3u;  // one register set per entry (PF = 2)
 std::atomic<uint32_t> g_plan_small{kSmallMaxBytes};
+// Entries shorter than this skip the chunks: plan_combine computes them, one thread each. Longer
+// bounds cost more than they save on config 3's Zipf mix: 128 B took 36 us off the chunk kernel
+// and added 54 us to combine (random slice-by-16 lookups from 64 lanes conflict in LDS banks).
+#ifndef BKD_PLAN_SERIAL
+#define BKD_PLAN_SERIAL 16
+#endif
+std::atomic<uint32_t> g_plan_serial{BKD_PLAN_SERIAL};
 #ifndef BKD_SHORT_MEAN_MAX
 #define BKD_SHORT_MEAN_MAX 1024
 #endif
@@ -367,6 +374,7 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     pg.ch = pg.step * pg.jc;
     pg.mis = (uint32_t)((uintptr_t)base & 127u);
     pg.merge = (uint32_t)g_plan_merge.load();
+    pg.serial = g_plan_serial.load();
     pg.nbins = (pg.ch + pg.merge - 1u + pg.step - 1u) / pg.step + 1u;
     pg.step_sh = (uint32_t)__builtin_ctz(pg.step);
     pg.ch_sh = (pg.ch & (pg.ch - 1u)) == 0u ? (uint32_t)__builtin_ctz(pg.ch) : 0xFFu;
@@ -446,7 +454,7 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     }
     const uint32_t* btab = tab + bkd::gf2::byte_table_offset(G);
     hipLaunchKernelGGL(bkd::plan_combine_kernel, dim3(std::min(nb * reps, pgrid)), dim3(1024), 0, st, base, offsets, lengths, seeds,
-                       seed_all, size, n, pg, xtab, bkd::gf2::xpow(algo, 8ull * pg.ch), tab + 1024, btab, ds.xinv[algo],
+                       seed_all, size, n, pg, xtab, bkd::gf2::xpow(algo, 8ull * pg.ch), btab, ds.xinv[algo],
                        bkd::gf2::poly(algo), pslot, partials, out, err, reps, blive, nb, run);
     e = hipGetLastError();
     if (e != hipSuccess) return fail(BKD_ERR_HIP, std::string("plan kernels: ") + hipGetErrorString(e));
@@ -1012,6 +1020,13 @@ int bkd_set_plan_small(uint32_t max_bytes) {
     if (max_bytes > kSmallMaxBytes || (max_bytes && max_bytes < 16u))
         return fail(BKD_ERR_INVALID_ARG, "short-entry class bound must be 0 or 16.." + std::to_string(kSmallMaxBytes));
     g_plan_small.store(max_bytes);
+    return BKD_OK;
+}
+
+int bkd_set_plan_serial(uint32_t max_bytes) {
+    if (max_bytes < 16u || max_bytes > bkd::kSerialMax)
+        return fail(BKD_ERR_INVALID_ARG, "serial bound must be 16.." + std::to_string(bkd::kSerialMax));
+    g_plan_serial.store(max_bytes);
     return BKD_OK;
 }
 

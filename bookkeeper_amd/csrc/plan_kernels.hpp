@@ -47,7 +47,11 @@ struct PlanGeo {
     uint32_t step_sh;  // log2(step)
     uint32_t ch_sh;    // log2(ch) when ch is a power of two, else 0xFF (64-bit divisions are slow)
     uint32_t small;    // entries of <= small bytes belong to the short-entry launch (0: none do)
+    uint32_t serial;   // entries shorter than this (16 .. kSerialMax) are computed by plan_combine
 };
+
+// Longest entry plan_combine computes itself, one thread per entry (serial_crc).
+constexpr uint32_t kSerialMax = 256u;
 
 // hdr words
 constexpr int kHdrTotal = 0;  // all chunks
@@ -86,7 +90,7 @@ __device__ __forceinline__ EntryPlan plan_entry(uint64_t o, uint32_t l, uint64_t
     p.e = (int64_t)(o + l);
     // chunk ends sit on 128-byte lines: a line is then never split between two chunks that run
     // at different times (each would fetch it from HBM)
-    if (l < 16u) {
+    if (l < pg.serial) {  // plan_combine, one thread per entry (at least every l < 16)
         p.kind = 1;
         return p;
     }
@@ -442,6 +446,74 @@ __device__ __forceinline__ uint32_t gf_pow_bits(uint32_t x, uint32_t e, uint32_t
 constexpr uint32_t kCombineSerial = 64;
 constexpr uint32_t kCombineWave = 4096;
 
+// Slice-by-16 tables in LDS: T[k * 256 + b] = byte b followed by k zero bytes; T[0 .. 255] is the
+// byte table. The reference's scalar fallback is the byte-at-a-time form of the same arithmetic
+// (circe ReflectedIntCrc / crc32c_sse42.cpp's table path).
+__device__ __forceinline__ void build_slice16(uint32_t* T, const uint32_t* __restrict__ btab) {
+    for (int b = threadIdx.x; b < 256; b += blockDim.x) T[b] = btab[b];
+    __syncthreads();
+    for (int b = threadIdx.x; b < 256; b += blockDim.x) {
+        uint32_t v = T[b];
+        for (int k = 1; k < 16; ++k) {
+            v = (v >> 8) ^ T[v & 0xffu];
+            T[k * 256 + b] = v;
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t fold4_t(const uint32_t* T, uint32_t reg, uint32_t w) {
+    const uint32_t c = reg ^ w;
+    return xor3(T[3 * 256 + (c & 0xffu)], T[2 * 256 + ((c >> 8) & 0xffu)], T[256 + ((c >> 16) & 0xffu)] ^ T[c >> 24]);
+}
+
+// Raw register of base[o, o + l) (1 <= l < kSerialMax) from `reg`, one thread: every 16-byte block
+// holding an entry byte is loaded at once (never a byte past those blocks), 16-byte windows of the
+// entry are cut from consecutive blocks (dword select + v_alignbyte) and folded slice-by-16 — only
+// the four lookups of the register's own bytes sit on the dependency chain.
+__device__ __forceinline__ uint32_t serial_crc(const uint8_t* __restrict__ base, uint64_t o, uint32_t l, uint32_t reg,
+                                               const uint32_t* T) {
+    constexpr int kMaxBlk = (int)(kSerialMax + 30u) / 16;
+    const uintptr_t pa = (uintptr_t)(base + o);
+    const u32x4* blk = reinterpret_cast<const u32x4*>(pa & ~(uintptr_t)15);
+    const uint32_t d = (uint32_t)(pa & 15u), s = d >> 2, sb = d & 3u;
+    const uint32_t nb = (d + l + 15u) >> 4, nw = l >> 4, t = l & 15u;
+    u32x4 b[kMaxBlk];
+#pragma unroll
+    for (int k = 0; k < kMaxBlk; ++k) b[k] = (uint32_t)k < nb ? blk[k] : u32x4{0u, 0u, 0u, 0u};
+    auto window = [&](const u32x4& lo, const u32x4& hi, uint32_t (&w)[4]) {
+        const uint32_t e[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        uint32_t v[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) v[i] = s == 0u ? e[i] : s == 1u ? e[i + 1] : s == 2u ? e[i + 2] : e[i + 3];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w[i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], sb);
+    };
+#pragma unroll
+    for (int j = 0; j + 1 < kMaxBlk; ++j) {
+        uint32_t w[4];
+        window(b[j], b[j + 1], w);
+        if ((uint32_t)j < nw) {
+            const uint32_t c = reg ^ w[0];
+            const uint32_t rest = xor3(xor3(T[11 * 256 + (w[1] & 0xffu)], T[10 * 256 + ((w[1] >> 8) & 0xffu)],
+                                            T[9 * 256 + ((w[1] >> 16) & 0xffu)] ^ T[8 * 256 + (w[1] >> 24)]),
+                                       xor3(T[7 * 256 + (w[2] & 0xffu)], T[6 * 256 + ((w[2] >> 8) & 0xffu)],
+                                            T[5 * 256 + ((w[2] >> 16) & 0xffu)] ^ T[4 * 256 + (w[2] >> 24)]),
+                                       xor3(T[3 * 256 + (w[3] & 0xffu)], T[2 * 256 + ((w[3] >> 8) & 0xffu)],
+                                            T[256 + ((w[3] >> 16) & 0xffu)] ^ T[w[3] >> 24]));
+            reg = xor3(xor3(T[15 * 256 + (c & 0xffu)], T[14 * 256 + ((c >> 8) & 0xffu)],
+                            T[13 * 256 + ((c >> 16) & 0xffu)] ^ T[12 * 256 + (c >> 24)]), rest, 0u);
+        } else if ((uint32_t)j == nw && t) {  // the last t < 16 bytes: whole dwords, then bytes
+            const uint32_t q = t >> 2;
+            if (q > 0u) reg = fold4_t(T, reg, w[0]);
+            if (q > 1u) reg = fold4_t(T, reg, w[1]);
+            if (q > 2u) reg = fold4_t(T, reg, w[2]);
+            uint32_t x = q == 0u ? w[0] : q == 1u ? w[1] : q == 2u ? w[2] : w[3];
+            for (uint32_t k = 0; k < (t & 3u); ++k, x >>= 8) reg = T[(reg ^ x) & 0xffu] ^ (reg >> 8);
+        }
+    }
+    return reg;
+}
+
 __device__ __forceinline__ uint32_t mul_x(const uint32_t* X, uint32_t r) {
     return xor3(X[r & 0xffu], X[256 + ((r >> 8) & 0xffu)], X[512 + ((r >> 16) & 0xffu)] ^ X[768 + (r >> 24)]);
 }
@@ -449,7 +521,7 @@ __device__ __forceinline__ uint32_t mul_x(const uint32_t* X, uint32_t r) {
 __global__ void __launch_bounds__(1024) plan_combine_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ lengths,
     const uint32_t* __restrict__ seeds, uint32_t seed_all, uint64_t size, uint64_t n, PlanGeo pg,
-    const uint32_t* __restrict__ xtab, uint32_t xval, const uint32_t* __restrict__ x32tab,
+    const uint32_t* __restrict__ xtab, uint32_t xval,
     const uint32_t* __restrict__ btab, const uint32_t* __restrict__ xinv, uint32_t poly,
     const uint32_t* __restrict__ pslot, const uint32_t* __restrict__ partials, uint32_t* __restrict__ out,
     uint32_t* __restrict__ err, uint32_t reps, const uint32_t* __restrict__ blive, uint32_t nblk, PlanRun run) {
@@ -459,15 +531,13 @@ __global__ void __launch_bounds__(1024) plan_combine_kernel(
     // Grid stride over the virtual blocks; the operator tables are staged once per block.
     if (!run.on()) return;
     __shared__ uint32_t X[1024];
-    __shared__ uint32_t W[1024];
-    __shared__ uint32_t B[256];
+    __shared__ uint32_t T[16 * 256];  // slice-by-16 (serial entries)
     __shared__ uint32_t big[1024];
     __shared__ uint32_t wsum[kPlanBlock / 64 + 1];
     __shared__ uint32_t nbig;
     __shared__ uint32_t red[1024 / 64];
     for (int k = threadIdx.x; k < 1024; k += blockDim.x) X[k] = xtab[k];
-    for (int k = threadIdx.x; k < 1024; k += blockDim.x) W[k] = x32tab[k];
-    for (int k = threadIdx.x; k < 256; k += blockDim.x) B[k] = btab[k];
+    build_slice16(T, btab);
     const uint32_t nvb = nblk * reps;
     for (uint32_t vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
     const uint32_t eb = vb / reps, rep = vb - eb * reps;
@@ -484,17 +554,8 @@ __global__ void __launch_bounds__(1024) plan_combine_kernel(
             out[i] = 0u;
             if (err) atomicOr(err, 1u);
         } else if (slot == kSerial) {
-            uint32_t reg = ~(seeds ? seeds[i] : seed_all);
-            const uint8_t* q = base + o;
-            const uint8_t* qe = q + l;
-            // bytes up to a 4-byte boundary, aligned dwords by x^32, trailing bytes
-            while (q < qe && ((uintptr_t)q & 3u)) reg = B[(reg ^ *q++) & 0xffu] ^ (reg >> 8);
-            for (; qe - q >= 4; q += 4) {
-                const uint32_t r = reg ^ *reinterpret_cast<const uint32_t*>(q);
-                reg = W[r & 0xffu] ^ W[256 + ((r >> 8) & 0xffu)] ^ W[512 + ((r >> 16) & 0xffu)] ^ W[768 + (r >> 24)];
-            }
-            while (q < qe) reg = B[(reg ^ *q++) & 0xffu] ^ (reg >> 8);
-            out[i] = ~reg;
+            const uint32_t reg = ~(seeds ? seeds[i] : seed_all);
+            out[i] = l ? ~serial_crc(base, o, l, reg, T) : ~reg;
         } else {
             const EntryPlan p = plan_entry(o, l, size, pg);
             if (p.m > kCombineSerial) {

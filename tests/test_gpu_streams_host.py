@@ -308,3 +308,37 @@ def test_plan_near_uniform_lengths(gpu, lo, hi):
         assert e.value.code == -4
     finally:
         ck.set_plan_mode(0)
+
+
+@pytest.mark.parametrize("serial", [16, 128, 256])
+def test_plan_serial_entries(gpu, serial):
+    """Plan entries shorter than the serial bound are computed by the combine kernel, one thread each
+    (slice-by-16 over windows cut from aligned 16-byte blocks): every length 0..300 at every start
+    alignment mod 16, seeded, both algorithms, plus an entry ending at the buffer's last byte."""
+    import torch
+    rng = np.random.default_rng(serial)
+    lens = np.tile(np.arange(0, 301), 16).astype(np.int64)
+    offs = rng.integers(0, 1 << 20, lens.size).astype(np.int64)
+    offs = offs - (offs & 15) + np.repeat(np.arange(16), 301)  # every alignment for every length
+    size = (1 << 20) + 512
+    lens = np.concatenate([lens, [200, 255]])
+    offs = np.concatenate([offs, [size - 200, size - 255]])  # last bytes of the buffer
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    seeds = rng.integers(0, 2**32, lens.size, dtype=np.uint64).astype(np.uint32)
+    base = _dev(torch, host, gpu)
+    d_seeds = _dev(torch, seeds.view(np.int32), gpu)
+    ck.set_plan_mode(2)
+    ck.set_plan_small(0)
+    ck.set_plan_serial(serial)
+    try:
+        for algo in (0, 1):
+            want = oracle.batch(algo, host, offs.astype(np.uint64), lens.astype(np.uint32), seeds=seeds)
+            out = ck.crc_batch(algo, base, _dev(torch, offs, gpu), _dev(torch, lens.astype(np.int32), gpu),
+                               seeds=d_seeds, sync_check=True)
+            got = out.cpu().numpy().view(np.uint32)
+            bad = np.nonzero(got != want)[0]
+            assert bad.size == 0, (algo, lens[bad[:5]], offs[bad[:5]] & 15)
+    finally:
+        ck.set_plan_mode(0)
+        ck.set_plan_small(192)
+        ck.set_plan_serial(16)
