@@ -4,7 +4,8 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}; O=$R/gpurun_out/pmci; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-LIBS="$R/bookkeeper_amd/libbkdigest.so $(ls $R/tools/variants_tmp/lib_c*.so)"
+LIBS="$R/bookkeeper_amd/libbkdigest.so"
+for i in 1 2 3 4 5; do cp $R/bookkeeper_amd/libbkdigest.so $O/lib_c$i.so; LIBS="$LIBS $O/lib_c$i.so"; done
 i=0
 for C in "SQC_ICACHE_MISSES SQC_ICACHE_HITS SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH SQ_WAIT_INST_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE" \
          "TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_STALL_MULTI_MISS_sum TCP_UTCL1_SERIALIZATION_STALL_sum GRBM_GUI_ACTIVE GRBM_UTCL2_BUSY" \
