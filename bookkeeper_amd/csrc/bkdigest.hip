@@ -790,7 +790,8 @@ int package_framed(DeviceState& ds, hipStream_t st, int algo, int64_t ledger_id,
         if (e != hipSuccess) return fail(BKD_ERR_NOMEM, std::string("bounds flag: ") + hipGetErrorString(e));
     }
     const unsigned blocks = (unsigned)((n + 255) / 256);
-    hipLaunchKernelGGL(bkd::package_header_kernel, dim3(blocks), dim3(256), 0, st, tab + 1024, ledger_id, d_entry_ids,
+    const unsigned hblocks = (unsigned)std::min<uint64_t>((n + 1023) / 1024, 2u * (uint64_t)ds.cus);
+    hipLaunchKernelGGL(bkd::package_header_kernel, dim3(hblocks), dim3(1024), 0, st, tab + 1024, ledger_id, d_entry_ids,
                        d_lacs, d_length_fields, n, (uint8_t*)d_frames, frame_stride, d_digests);
     BKD_HIP(hipGetLastError());
     bkd::IndexedSrc src{n, d_offsets, d_lengths, d_digests, 0u, payload_size, d_digests};
@@ -827,7 +828,8 @@ int verify_framed(DeviceState& ds, hipStream_t st, int algo, int64_t ledger_id, 
     uint64_t* poff = Carver::at<uint64_t>(sb, o_poff);
     uint32_t* expect = Carver::at<uint32_t>(sb, o_exp);
     uint32_t* pre = Carver::at<uint32_t>(sb, o_pre);
-    hipLaunchKernelGGL(bkd::verify_header_kernel, dim3(blocks), dim3(256), 0, st, x32tab, (const uint8_t*)d_framed,
+    const unsigned hblocks = (unsigned)std::min<uint64_t>((n + 1023) / 1024, 2u * (uint64_t)ds.cus);
+    hipLaunchKernelGGL(bkd::verify_header_kernel, dim3(hblocks), dim3(1024), 0, st, x32tab, (const uint8_t*)d_framed,
                        framed_size, d_offsets, d_lengths, n, mac, ledger_id, first_entry_id, id_checks, seeds, poff,
                        plen, expect, pre, d_first_bad);
     e = hipGetLastError();

@@ -52,11 +52,18 @@ def main(paths):
     lt = lens < 1024
     head_l = np.where(lens % 4096 == 0, 4096, lens % 4096)  # what the plan leaves as heads, packed alone
     head_o = np.concatenate([[0], np.cumsum(head_l[:-1])])
+    hs_l = np.sort(head_l)[::-1]  # the same heads packed in the plan's processing order (longest first)
+    hs_o = np.concatenate([[0], np.cumsum(hs_l[:-1])])
+    m1_l = np.where(np.arange(n) % 256 == 0, 2048, 1024)  # 1 KiB chunks through the plan (outside the gate's band)
+    m1_o = np.concatenate([[0], np.cumsum(m1_l[:-1])])
     work = {
         "zipf": (0, *idx(offs, lens), total),
         "zipf_crc32": (1, *idx(offs, lens), total),
         "zipf_lt1k": (0, *idx(offs[lt], lens[lt]), int(lens[lt].sum())),
         "zipf_heads": (0, *idx(head_o, head_l), int(head_l.sum())),
+        "zipf_heads_sorted": (0, *idx(hs_o, hs_l), int(hs_l.sum())),
+        "mixed1k": (0, *idx(m1_o, m1_l), int(m1_l.sum())),
+        "uniform1k_idx": (0, *idx(np.arange(n) * 1024, np.full(n, 1024)), n * 1024),
         "packed64": (0, *idx(np.arange(n) * 64, np.full(n, 64)), n * 64),
         "packed64_64m": (0, *idx(np.arange(64 * n) * 64, np.full(64 * n, 64)), 64 * n * 64),
         "indexed4k": (0, *idx(np.arange(n) * 4096, np.full(n, 4096)), n * 4096),
@@ -70,7 +77,38 @@ def main(paths):
     out = torch.empty(max(n, max((4 << 30) // S for S, _ in small.values())), dtype=torch.int32, device=dev)
     assert base.numel() >= 4 << 30
 
+    fr = {}
+
+    def framed():  # 1M framed 4 KiB entries (CRC32C: 32 B header + 4 B digest + payload), packaged once
+        if not fr:
+            F = torch.empty(n * 4096, dtype=torch.uint8, device=dev)
+            first.bkd_fill_splitmix64(ptr(F), F.numel(), 7, 0, None)
+            ids = torch.arange(n, dtype=torch.int64, device=dev)
+            fr.update(F=F, ids=ids, lacs=ids - 1, lenf=torch.full((n,), 4096 - 36, dtype=torch.int64, device=dev),
+                      poff=ids * 4096 + 36, plen=torch.full((n,), 4096 - 36, dtype=torch.int32, device=dev),
+                      foff=ids * 4096, flen=torch.full((n,), 4096, dtype=torch.int32, device=dev),
+                      dig=torch.empty(n, dtype=torch.int32, device=dev),
+                      status=torch.empty(n, dtype=torch.int32, device=dev),
+                      fb=torch.empty(1, dtype=torch.int64, device=dev))
+            package(first)
+            torch.cuda.synchronize()
+        return fr
+
+    def package(L):
+        f = fr
+        return L.bkd_digest_package_batch(0, 7, ptr(f["ids"]), ptr(f["lacs"]), ptr(f["lenf"]), ptr(f["F"]),
+                                          f["F"].numel(), ptr(f["poff"]), ptr(f["plen"]), n, ptr(f["F"]), 4096,
+                                          ptr(f["dig"]), ctypes.c_void_p(st.cuda_stream))
+
     def call(L, name):
+        if name == "package4k":
+            framed()
+            return package(L)
+        if name == "verify4k":
+            f = framed()
+            r = L.bkd_digest_verify_batch(0, 7, 0, 0, ptr(f["F"]), f["F"].numel(), ptr(f["foff"]), ptr(f["flen"]), n,
+                                          ptr(f["status"]), ptr(f["fb"]), ctypes.c_void_p(st.cuda_stream))
+            return r
         if name == "uniform4k":
             L.bkd_set_group_lanes(0)
             return L.bkd_crc_batch_uniform(0, ptr(base), 4096, 4096, n, None, 0, ptr(out), ctypes.c_void_p(st.cuda_stream))
@@ -94,6 +132,8 @@ def main(paths):
             assert call(L, name) == 0, name
             torch.cuda.synchronize()
             cnt = work[name][1].numel() if name in work else ((4 << 30) // small[name][0] if name in small else n)
+            if name in ("package4k", "verify4k"):
+                out[:n].copy_(fr["dig"] if name == "package4k" else fr["status"])
             if ref is None:
                 ref = out[:cnt].clone()
             assert torch.equal(out[:cnt], ref), f"{name}: digests differ between libraries"
