@@ -317,7 +317,7 @@ def set_plan_small(max_bytes: int = 192) -> None:
 
 
 def set_plan_serial(max_bytes: int = 16) -> None:
-    """Plan entries shorter than max_bytes (16..256) are computed by the combine kernel, one thread each."""
+    """Plan entries shorter than max_bytes (16..64) are computed by the combine kernel, one thread each."""
     check(lib().bkd_set_plan_serial(max_bytes))
 
 

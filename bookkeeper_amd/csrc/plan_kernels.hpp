@@ -51,7 +51,7 @@ struct PlanGeo {
 };
 
 // Longest entry plan_combine computes itself, one thread per entry (serial_crc).
-constexpr uint32_t kSerialMax = 256u;
+constexpr uint32_t kSerialMax = 64u;
 
 // hdr words
 constexpr int kHdrTotal = 0;  // all chunks
@@ -275,7 +275,12 @@ __device__ __forceinline__ PlanDesc chunk_desc_of(int64_t ae, int64_t s0, uint32
 // chunks of the block's entries form one contiguous run in the full bin, written by the whole
 // block (one descriptor per thread per pass, coalesced, no per-entry serial loop) — including
 // entries with thousands of chunks. Grid stride over the nb * reps virtual blocks.
-__global__ void __launch_bounds__(kPlanBlock) plan_emit_kernel(const uint64_t* __restrict__ offsets,
+#ifndef BKD_PLAN_OCC
+#define BKD_PLAN_OCC 8
+#endif
+// emit and combine at 8 waves per SIMD (<= 64 VGPRs): two 1024-thread blocks per CU resident, as
+// BKD_PLAN_GRID launches them
+__global__ void __launch_bounds__(kPlanBlock, BKD_PLAN_OCC) plan_emit_kernel(const uint64_t* __restrict__ offsets,
                                                                const uint32_t* __restrict__ lengths,
                                                                const uint32_t* __restrict__ seeds, uint32_t seed_all,
                                                                uint64_t size, uint64_t n, PlanGeo pg,
@@ -518,7 +523,7 @@ __device__ __forceinline__ uint32_t mul_x(const uint32_t* X, uint32_t r) {
     return xor3(X[r & 0xffu], X[256 + ((r >> 8) & 0xffu)], X[512 + ((r >> 16) & 0xffu)] ^ X[768 + (r >> 24)]);
 }
 
-__global__ void __launch_bounds__(1024) plan_combine_kernel(
+__global__ void __launch_bounds__(1024, BKD_PLAN_OCC) plan_combine_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ lengths,
     const uint32_t* __restrict__ seeds, uint32_t seed_all, uint64_t size, uint64_t n, PlanGeo pg,
     const uint32_t* __restrict__ xtab, uint32_t xval,

@@ -256,7 +256,7 @@ BKD_API int bkd_set_plan_geometry(int lanes, int steps_per_chunk, int merge_byte
  * one, and skip the plan's count/emit/chunk/combine work. Used when the base buffer
  * holds at most 1 KiB per entry (short entries dominate). Default 192. */
 BKD_API int bkd_set_plan_small(uint32_t max_bytes);
-/* Entries of the plan shorter than `bytes` (16..256, default 16) skip the chunk kernel: the
+/* Entries of the plan shorter than `bytes` (16..64, default 16) skip the chunk kernel: the
  * combine kernel computes each with one thread (slice-by-16 over its 16-byte windows). */
 BKD_API int bkd_set_plan_serial(uint32_t bytes);
 /* Register double-buffer depth of the plan's chunk kernel (2, 4 or 8 loads per lane). */

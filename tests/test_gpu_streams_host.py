@@ -310,7 +310,7 @@ def test_plan_near_uniform_lengths(gpu, lo, hi):
         ck.set_plan_mode(0)
 
 
-@pytest.mark.parametrize("serial", [16, 128, 256])
+@pytest.mark.parametrize("serial", [16, 40, 64])
 def test_plan_serial_entries(gpu, serial):
     """Plan entries shorter than the serial bound are computed by the combine kernel, one thread each
     (slice-by-16 over windows cut from aligned 16-byte blocks): every length 0..300 at every start
