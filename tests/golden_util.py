@@ -10,6 +10,17 @@ def load():
     return json.load(open(GOLDEN))
 
 
+def load_4096():
+    """The 4096-entry seeded set (lengths 0..70000, unaligned offsets into a 32 MiB stream)."""
+    import numpy as np
+    d = json.load(open(os.path.join(os.path.dirname(GOLDEN), "crc_golden_4096.json")))
+    for k in ("offsets",):
+        d[k] = np.array(d[k], dtype=np.uint64)
+    for k in ("lengths", "seeds", "crc32c", "crc32"):
+        d[k] = np.array(d[k], dtype=np.uint32)
+    return d
+
+
 def literal_bytes(v) -> bytes:
     if v.get("hex") is not None:
         return bytes.fromhex(v["hex"])

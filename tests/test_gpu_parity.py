@@ -99,6 +99,27 @@ def test_golden_vectors(gpu):
         assert (got == want).all(), lanes
 
 
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_golden_batch_4096(gpu, mode):
+    """SURVEY.md §8c's 4096-entry reference-generated set (lengths 0..70000, unaligned offsets into
+    a 32 MiB stream, seeded) through the automatic route, the direct kernel and the chunk plan."""
+    import torch
+    fx = golden_util.load_4096()
+    data = oracle.fill_splitmix64(fx["bytes"], fx["seed"])
+    base = _dev_bytes(torch, data, gpu)
+    offs = torch.from_numpy(fx["offsets"].astype(np.int64)).to(gpu)
+    lens = torch.from_numpy(fx["lengths"].view(np.int32)).to(gpu)
+    seeds = torch.from_numpy(fx["seeds"].view(np.int32)).to(gpu)
+    ck.set_plan_mode(mode)
+    try:
+        for algo, key in ((ck.CRC32C, "crc32c"), (ck.CRC32, "crc32")):
+            got = ck.crc_batch(algo, base, offs, lens, seeds=seeds, sync_check=True).cpu().numpy().view(np.uint32)
+            bad = np.nonzero(got != fx[key])[0]
+            assert bad.size == 0, (key, bad[:5])
+    finally:
+        ck.set_plan_mode(0)
+
+
 def test_fill_splitmix64_matches_oracle(gpu):
     import torch
     for nbytes, first in [(4096, 0), (1000003, 17), (8, 5)]:

@@ -85,6 +85,18 @@ def test_cpu_route_against_golden_and_oracle(algo):
     assert ck.cpu_impl() in ("vpclmul512+pclmul+sse4.2", "pclmul+sse4.2", "pclmul", "slice8")
 
 
+@pytest.mark.parametrize("algo", [0, 1])
+def test_cpu_route_golden_4096(algo):
+    """The CPU route against the 4096-entry reference-generated set (lengths 0..70000, seeded)."""
+    import golden_util
+    fx = golden_util.load_4096()
+    data = oracle.fill_splitmix64(fx["bytes"], fx["seed"])
+    key = "crc32c" if algo == 0 else "crc32"
+    for i in range(len(fx["lengths"])):
+        o, n = int(fx["offsets"][i]), int(fx["lengths"][i])
+        assert ck.cpu_resume(algo, int(fx["seeds"][i]), data[o:o + n]) & 0xFFFFFFFF == int(fx[key][i]), i
+
+
 def test_cpu_route_threshold_setting():
     old = ck.get_cpu_route_max()
     try:

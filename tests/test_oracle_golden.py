@@ -53,6 +53,14 @@ def test_golden_batch():
     assert (got == np.array([int(x, 16) for x in fx["crc32"]], dtype=np.uint32)).all()
 
 
+def test_golden_batch_4096():
+    """SURVEY.md §8c's larger fixture: 4096 seeded entries, lengths 0..70000, unaligned offsets."""
+    fx = golden_util.load_4096()
+    data = oracle.fill_splitmix64(fx["bytes"], fx["seed"])
+    assert (oracle.batch(oracle.CRC32C, data, fx["offsets"], fx["lengths"], seeds=fx["seeds"]) == fx["crc32c"]).all()
+    assert (oracle.batch(oracle.CRC32, data, fx["offsets"], fx["lengths"], seeds=fx["seeds"]) == fx["crc32"]).all()
+
+
 def test_survey_digest_frame_vectors():
     # SURVEY.md §8c rows restating DigestManager.java:146-153 with CompositeByteBufUnwrapBugReproduceTest inputs
     for size, c32c, c32 in [(16383, 0x24656066, 0xDF2EBB5B), (16384, 0x6FA1A26B, 0x4512B34E)]:
