@@ -56,6 +56,11 @@ def main(paths):
     hs_o = np.concatenate([[0], np.cumsum(hs_l[:-1])])
     ha_l = (hs_l + 127) // 128 * 128  # the sorted heads rounded up to whole 128-byte lines: no pad, no straddle
     ha_o = np.concatenate([[0], np.cumsum(ha_l[:-1])])
+    # the sorted heads, each in its own 128-byte lines (no line shared with a neighbour): starting on
+    # a line (heads_sep_al) or at its original offset within the line (heads_sep)
+    slot = (hs_l + 127 + 127) // 128 * 128
+    sep_base = np.concatenate([[0], np.cumsum(slot[:-1])])
+    hsep_al_o, hsep_o = sep_base, sep_base + (hs_o % 128)
     m1_l = np.where(np.arange(n) % 256 == 0, 2048, 1024)  # 1 KiB chunks through the plan (outside the gate's band)
     m1_o = np.concatenate([[0], np.cumsum(m1_l[:-1])])
     work = {
@@ -66,6 +71,8 @@ def main(paths):
         "zipf_heads_sorted": (0, *idx(hs_o, hs_l), int(hs_l.sum())),
         "mixed1k": (0, *idx(m1_o, m1_l), int(m1_l.sum())),
         "heads_aligned": (0, *idx(ha_o, ha_l), int(ha_l.sum())),
+        "heads_sep_al": (0, *idx(hsep_al_o, hs_l), int(hs_l.sum())),
+        "heads_sep": (0, *idx(hsep_o, hs_l), int(hs_l.sum())),
         "uniform1k_idx": (0, *idx(np.arange(n) * 1024, np.full(n, 1024)), n * 1024),
         "packed64": (0, *idx(np.arange(n) * 64, np.full(n, 64)), n * 64),
         "packed64_64m": (0, *idx(np.arange(64 * n) * 64, np.full(64 * n, 64)), 64 * n * 64),
