@@ -920,42 +920,35 @@ __device__ __forceinline__ void plan_chunks_loop(const uint32_t* lds, uint32_t l
     u32x4 W0x, Ax[PF], Bx[PF], W0y, Ay[PF], By[PF];
     uint64_t i = gid;
     ChunkGeo cur = chunk_geo<G>(descs[i], g);
-    PlanDesc dn = descs[clampi(i + ngroups)];
+    // Descriptors of the next chunk of each half live in their own registers (dA for set-X halves,
+    // dB for set-Y halves), each loaded two halves before its use and reloaded (three rounds ahead)
+    // right after: no copy of a just-loaded value (a `dn = dnn` copy made the compiler wait for that
+    // load), and enough loads issued between a descriptor and its use that the compiler's count of
+    // them never reaches back into the current chunk's prefetch.
+    PlanDesc dA = descs[clampi(i + ngroups)], dB = descs[clampi(i + 2 * ngroups)];
     ChunkGeo safe = cur;
     if (!cur.len) safe.la0 = safe.a = 0, safe.J = 1;  // hole first: prefetch base[0..16)
     chunk_prefetch<G, PF, NT>(base, cur.len ? cur : safe, W0x, Ax);
-    for (;;) {
-        {  // chunk i in set X, prefetch into Y
-            const PlanDesc dnn = descs[clampi(i + 2 * ngroups)];
-            const bool more = i + ngroups < n;
-            ChunkGeo nx = chunk_geo<G>(dn, g);
-            if (!more) nx.len = 0;
-            const ChunkGeo& pg = pf_geo(nx, cur.len ? cur : safe);
-            const uint32_t v = cur.len ? chunk_fold<G, PF, NT>(lds, lanereg, g, base, cur, W0x, Ax, Bx, pg, W0y, Ay)
-                                       : (chunk_prefetch<G, PF, NT>(base, pg, W0y, Ay), 0u);
-            emit(cur, v);
-            if (!more) break;
-            i += ngroups;
-            if (cur.len) safe = cur;
-            cur = nx;
-            dn = dnn;
-        }
-        {  // chunk i in set Y, prefetch into X
-            const PlanDesc dnn = descs[clampi(i + 2 * ngroups)];
-            const bool more = i + ngroups < n;
-            ChunkGeo nx = chunk_geo<G>(dn, g);
-            if (!more) nx.len = 0;
-            const ChunkGeo& pg = pf_geo(nx, cur.len ? cur : safe);
-            const uint32_t v = cur.len ? chunk_fold<G, PF, NT>(lds, lanereg, g, base, cur, W0y, Ay, By, pg, W0x, Ax)
-                                       : (chunk_prefetch<G, PF, NT>(base, pg, W0x, Ax), 0u);
-            emit(cur, v);
-            if (!more) break;
-            i += ngroups;
-            if (cur.len) safe = cur;
-            cur = nx;
-            dn = dnn;
-        }
+#define BKD_CHUNK_HALF(DN, W0C, AC, BC, W0N, AN)                                                            \
+    {                                                                                                      \
+        const bool more = i + ngroups < n;                                                                 \
+        ChunkGeo nx = chunk_geo<G>(DN, g);                                                                 \
+        DN = descs[clampi(i + 3 * ngroups)];                                                               \
+        if (!more) nx.len = 0;                                                                             \
+        const ChunkGeo& pg = pf_geo(nx, cur.len ? cur : safe);                                             \
+        const uint32_t v = cur.len ? chunk_fold<G, PF, NT>(lds, lanereg, g, base, cur, W0C, AC, BC, pg, W0N, AN) \
+                                   : (chunk_prefetch<G, PF, NT>(base, pg, W0N, AN), 0u);                   \
+        emit(cur, v);                                                                                      \
+        if (!more) break;                                                                                  \
+        i += ngroups;                                                                                      \
+        if (cur.len) safe = cur;                                                                           \
+        cur = nx;                                                                                          \
     }
+    for (;;) {
+        BKD_CHUNK_HALF(dA, W0x, Ax, Bx, W0y, Ay)  // chunk i in set X, prefetch into Y
+        BKD_CHUNK_HALF(dB, W0y, Ay, By, W0x, Ax)  // chunk i in set Y, prefetch into X
+    }
+#undef BKD_CHUNK_HALF
 }
 
 // Per-block work queue over the sorted chunk list (BKD_SCHED=1): block b owns positions b, b + NB,
