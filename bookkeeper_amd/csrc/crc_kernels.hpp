@@ -715,14 +715,18 @@ __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __res
 }
 
 // ---- chunk descriptors of the ragged-batch plan (built by plan_kernels.hpp) ----
-// 16 bytes: s (41-bit byte offset) | pad (7 bits) | len (16 bits; a chunk is at most CH + 15 <
-// 64 KiB bytes), the register folded into its first bytes, and the destination (bit 31: finalized
-// CRC into out[dst], else raw partial into partials[dst]). len == 0 marks a hole (skipped).
-// pad > 0: the chunk [s, s+len) ends on a 128-byte line past its entry's end; its last pad bytes
-// belong to other data and are folded as zeros (the combine then multiplies by x^(-8*pad)).
+// 16 bytes: W + kWBias (41 bits; W = the byte offset where the chunk's step-aligned window starts,
+// up to one step before the chunk's first byte) | pad (7 bits) | len (16 bits; a chunk is at most
+// CH + 15 < 64 KiB bytes), the register folded into its first bytes, and the destination (bit 31:
+// finalized CRC into out[dst], else raw partial into partials[dst]). len == 0 marks a hole. The
+// chunk is [W + lead, W + J*step) with J = ceil(len / step), lead = J*step - len: the chunk kernel
+// derives each lane's masks from those small integers instead of 64-bit address arithmetic.
+// pad > 0: the chunk ends on a 128-byte line past its entry's end; its last pad bytes belong to
+// other data and are folded as zeros (the combine then multiplies by x^(-8*pad)).
 constexpr uint32_t kPlanFinal = 0x80000000u;
 constexpr int kPlanOffBits = 41;
-constexpr uint64_t kPlanMaxSize = 1ull << kPlanOffBits;
+constexpr uint64_t kPlanMaxSize = 1ull << (kPlanOffBits - 1);  // W + kWBias fits the 41 bits
+constexpr int64_t kWBias = 1024;                                 // > the widest step (64 lanes x 16 B)
 
 struct __attribute__((aligned(16))) PlanDesc {
     uint64_t s_len;
@@ -737,26 +741,31 @@ struct __attribute__((aligned(16))) PlanDesc {
 // set chunk k is not using, and no register copy (which would force a vmcnt wait) is needed.
 
 struct ChunkGeo {
-    int64_t s;    // first byte
-    int64_t a;    // this lane's step-0 address (16-byte aligned)
-    int64_t la0;  // step-0 load address: a, or the aligned block holding s for lanes before s
+    int64_t a;    // this lane's step-0 block (16-byte aligned)
+    int64_t la0;  // step-0 load address: a, or for windows wider than a line the block holding the
+                  // first byte (a lane's own block could then lie on the page before it)
     uint32_t J;   // steps
     uint32_t r0;  // register folded into the first bytes
     uint32_t dst;
     uint32_t len;
     uint32_t pad;  // trailing bytes of the window that are not the entry's (folded as zeros)
+    int32_t d0;    // bytes of this lane's step-0 block before the chunk's first byte (lead - 16g)
+    int32_t keep;  // bytes of this lane's last-step block that belong to the chunk (step - pad - 16g)
 };
 
 template <int G>
 __device__ __forceinline__ ChunkGeo chunk_geo(const PlanDesc& d, int g) {
+    using Gm = Geo<G>;
     ChunkGeo c;
-    c.s = (int64_t)(d.s_len & (kPlanMaxSize - 1u));
+    const int64_t w = (int64_t)(d.s_len & ((1ull << kPlanOffBits) - 1u)) - kWBias;
     c.pad = (uint32_t)(d.s_len >> kPlanOffBits) & 127u;
     c.len = (uint32_t)(d.s_len >> 48);
-    const int64_t e = c.s + (int64_t)c.len;
-    c.J = (uint32_t)((c.len + Geo<G>::kStep - 1) / Geo<G>::kStep);
-    c.a = e - (int64_t)c.J * Geo<G>::kStep + 16 * g;
-    c.la0 = c.a < c.s ? c.a + ((c.s - c.a) & ~(int64_t)15) : c.a;
+    c.J = (c.len + (uint32_t)Gm::kStep - 1u) / (uint32_t)Gm::kStep;  // a power of two: a shift
+    c.d0 = (int32_t)(c.J * (uint32_t)Gm::kStep - c.len) - 16 * g;
+    c.keep = Gm::kStep - (int32_t)c.pad - 16 * g;
+    c.a = w + 16 * g;
+    if constexpr (Gm::kStep > 128) c.la0 = c.d0 >= 16 ? c.a + (c.d0 & ~15) : c.a;
+    else c.la0 = c.a;  // the window's first step is one line, the line of the chunk's first byte
     c.r0 = d.r0;
     c.dst = d.dst;
     return c;
@@ -790,21 +799,21 @@ __device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lan
                                                u32x4 (&A)[PF], u32x4 (&B)[PF], const ChunkGeo& nx, u32x4& NW0,
                                                u32x4 (&NA)[PF]) {
     using Gm = Geo<G>;
-    const int64_t s = c.s, a = c.a;
+    const int64_t a = c.a;
+    const int32_t d0 = c.d0;
     u32x4 w;
-    if (a >= s) w = W0;
-    else if (a + 16 > s) w = mask_low_bytes(W0, (uint32_t)(s - a));
+    if (d0 <= 0) w = W0;
+    else if (d0 < 16) w = mask_low_bytes(W0, (uint32_t)d0);
     else w = u32x4{0u, 0u, 0u, 0u};
     const uint32_t r0 = c.r0;
-    if (a < s + 4 && a + 16 > s) {
-        const int64_t d = s - a;
-        w.x ^= place_seed(r0, d);
-        w.y ^= place_seed(r0, d - 4);
-        w.z ^= place_seed(r0, d - 8);
-        w.w ^= place_seed(r0, d - 12);
+    if (d0 > -4 && d0 < 16) {
+        w.x ^= place_seed(r0, d0);
+        w.y ^= place_seed(r0, d0 - 4);
+        w.z ^= place_seed(r0, d0 - 8);
+        w.w ^= place_seed(r0, d0 - 12);
     }
     uint32_t fx = 0u;
-    if (a + Gm::kStep < s + 4) fx = place_seed(r0, s - (a + Gm::kStep));
+    if (d0 > Gm::kStep - 4) fx = place_seed(r0, d0 - Gm::kStep);
     uint32_t c0 = w.x, c1 = w.y, c2 = w.z, c3 = w.w;
     const uint32_t rem = c.J - 1u;
 #define BKD_FOLD0(d)                                     \
@@ -870,9 +879,7 @@ __device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lan
     if (c.pad) {
         // the last step's block of this lane ends past the entry: its bytes >= the entry's end
         // were folded last (XORed in after the final multiply), so XOR them out again
-        const int64_t al = a + (int64_t)(c.J - 1u) * Gm::kStep;
-        const int64_t et = s + (int64_t)c.len - (int64_t)c.pad;
-        if (al + 16 > et) {
+        if (c.keep < 16) {
             u32x4 last;
             if (rem == 0u) {
                 last = W0;
@@ -890,7 +897,7 @@ __device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lan
                     if ((uint32_t)(PF + k) + 1u == left) last = A[k];
                 }
             }
-            const int64_t keep = et - al;
+            const int32_t keep = c.keep;
             const u32x4 junk = keep <= 0 ? last : mask_low_bytes(last, (uint32_t)keep);
             c0 ^= junk.x;
             c1 ^= junk.y;

@@ -121,7 +121,10 @@ __device__ __forceinline__ PlanDesc chunk_desc(const EntryPlan& p, uint32_t c, u
     const bool head = c + 1u == p.m;
     const int64_t s = head ? p.s : e - (int64_t)pg.ch;
     const uint64_t pad = c == 0u ? (uint64_t)p.pad : 0u;
-    d.s_len = (uint64_t)s | (pad << kPlanOffBits) | ((uint64_t)(e - s) << 48);
+    const uint32_t len = (uint32_t)(e - s);
+    const uint32_t J = (len + pg.step - 1u) >> pg.step_sh;
+    const int64_t w = e - (int64_t)J * (int64_t)pg.step;  // the chunk's step-aligned window start
+    d.s_len = (uint64_t)(w + kWBias) | (pad << kPlanOffBits) | ((uint64_t)len << 48);
     d.r0 = head ? ~seed : 0u;
     d.dst = p.ps == 0u ? (entry | kPlanFinal) : slot + c;
     return d;
