@@ -70,6 +70,9 @@ def main(paths):
         "zipf_heads": (0, *idx(head_o, head_l), int(head_l.sum())),
         "zipf_heads_sorted": (0, *idx(hs_o, hs_l), int(hs_l.sum())),
         "mixed1k": (0, *idx(m1_o, m1_l), int(m1_l.sum())),
+        # 1 M chunks of 1 / 2 / 4 steps through the plan (one 4 KiB entry keeps them out of the gate's band)
+        **{f"chunk{k}s": (0, *idx(np.arange(n) * 1024 + 7, np.where(np.arange(n) == 5, 4096, 128 * k - 28)),
+                          n * (128 * k - 28)) for k in (1, 2, 4)},
         "heads_aligned": (0, *idx(ha_o, ha_l), int(ha_l.sum())),
         "heads_sep_al": (0, *idx(hsep_al_o, hs_l), int(hs_l.sum())),
         "heads_sep": (0, *idx(hsep_o, hs_l), int(hs_l.sum())),
