@@ -394,7 +394,7 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     const size_t o_blk = cv.take((size_t)nb * ncols * 4), o_live = cv.take((size_t)nb * 4),
                  o_bok = cv.take((size_t)nb * 4),
                  o_blkoff = cv.take((size_t)nb * ncols * 4), o_hdr = cv.take(bkd::kHdrWords * 4),
-                 o_ps = cv.take((size_t)n * 4), o_part = cv.take((size_t)capacity * 4),
+                 o_ps = cv.take((size_t)n * 4), o_hs = cv.take((size_t)n * 4), o_part = cv.take((size_t)capacity * 4),
                  o_desc = cv.take((size_t)capacity * sizeof(bkd::PlanDesc));
     StreamScratch& sc = scratch_for(ds, st);
     std::lock_guard<std::recursive_mutex> lk(sc.mu);
@@ -420,7 +420,8 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     uint32_t *blk = Carver::at<uint32_t>(sb, o_blk), *blive = Carver::at<uint32_t>(sb, o_live),
              *bok = gate ? Carver::at<uint32_t>(sb, o_bok) : nullptr,
              *blkoff = Carver::at<uint32_t>(sb, o_blkoff), *hdr = Carver::at<uint32_t>(sb, o_hdr),
-             *pslot = Carver::at<uint32_t>(sb, o_ps), *partials = Carver::at<uint32_t>(sb, o_part);
+             *pslot = Carver::at<uint32_t>(sb, o_ps), *hslot = Carver::at<uint32_t>(sb, o_hs),
+             *partials = Carver::at<uint32_t>(sb, o_part);
     bkd::PlanDesc* descs = Carver::at<bkd::PlanDesc>(sb, o_desc);
     if (pg.small) {  // the short-entry class, in its own launch (any order against the plan kernels)
         const bkd::SmallIndexedSrc ss{n, offsets, lengths, seeds, seed_all, size, out, pg.small, run_word, run.epoch};
@@ -442,7 +443,7 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     // few entry blocks (large entries): replicate emit and combine blocks so ~2 blocks per CU work
     const uint32_t reps = nb >= 2u * (uint32_t)ds.cus ? 1u : std::min<uint32_t>(64u, (2u * (uint32_t)ds.cus + nb - 1u) / nb);
     hipLaunchKernelGGL(bkd::plan_emit_kernel, dim3(std::min(nb * reps, pgrid)), dim3(bkd::kPlanBlock), 0, st, offsets,
-                       lengths, seeds, seed_all, size, n, pg, capacity, blkoff, pslot, hdr, descs, reps, blive, nb, run);
+                       lengths, seeds, seed_all, size, n, pg, capacity, blkoff, pslot, hslot, hdr, descs, reps, blive, nb, run);
     const uint32_t* tab = ds.tables[algo][lane_index(G)];
     const bkd::PlanDirectSrc ov{n, offsets, lengths, seeds, seed_all, size, out, pslot, hdr, capacity, false};
     switch (G) {
@@ -455,7 +456,7 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     const uint32_t* btab = tab + bkd::gf2::byte_table_offset(G);
     hipLaunchKernelGGL(bkd::plan_combine_kernel, dim3(std::min(nb * reps, pgrid)), dim3(1024), 0, st, base, offsets, lengths, seeds,
                        seed_all, size, n, pg, xtab, bkd::gf2::xpow(algo, 8ull * pg.ch), btab, ds.xinv[algo],
-                       bkd::gf2::poly(algo), pslot, partials, out, err, reps, blive, nb, run);
+                       bkd::gf2::poly(algo), pslot, hslot, partials, out, err, reps, blive, nb, run);
     e = hipGetLastError();
     if (e != hipSuccess) return fail(BKD_ERR_HIP, std::string("plan kernels: ") + hipGetErrorString(e));
     return BKD_OK;

@@ -126,7 +126,7 @@ __device__ __forceinline__ PlanDesc chunk_desc(const EntryPlan& p, uint32_t c, u
     const int64_t w = e - (int64_t)J * (int64_t)pg.step;  // the chunk's step-aligned window start
     d.s_len = (uint64_t)(w + kWBias) | (pad << kPlanOffBits) | ((uint64_t)len << 48);
     d.r0 = head ? ~seed : 0u;
-    d.dst = p.ps == 0u ? (entry | kPlanFinal) : slot + c;
+    d.dst = p.ps == 0u ? (entry | kPlanFinal) : slot;  // slot: the chunk's own list position
     return d;
 }
 
@@ -288,7 +288,8 @@ __global__ void __launch_bounds__(kPlanBlock, BKD_PLAN_OCC) plan_emit_kernel(con
                                                                const uint32_t* __restrict__ seeds, uint32_t seed_all,
                                                                uint64_t size, uint64_t n, PlanGeo pg,
                                                                uint64_t capacity, const uint32_t* __restrict__ blkoff,
-                                                               uint32_t* __restrict__ pslot, uint32_t* __restrict__ hdr,
+                                                               uint32_t* __restrict__ pslot, uint32_t* __restrict__ hslot,
+                                                               uint32_t* __restrict__ hdr,
                                                                PlanDesc* __restrict__ descs, uint32_t reps,
                                                                const uint32_t* __restrict__ blive, uint32_t nb,
                                                                PlanRun run) {
@@ -301,7 +302,7 @@ __global__ void __launch_bounds__(kPlanBlock, BKD_PLAN_OCC) plan_emit_kernel(con
     __shared__ uint32_t cursor[kMaxJC + 2];
     __shared__ uint32_t exf[kPlanBlock + 1];  // block-exclusive scan of full-chunk counts (+ total)
     __shared__ int64_t st_ae[kPlanBlock], st_s[kPlanBlock];
-    __shared__ uint32_t st_m[kPlanBlock], st_flags[kPlanBlock], st_seed[kPlanBlock], st_slot[kPlanBlock];
+    __shared__ uint32_t st_m[kPlanBlock], st_flags[kPlanBlock], st_seed[kPlanBlock];
     __shared__ uint32_t s_total;
     const uint32_t ncols = plan_ncols(pg);
     for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) bin0[k] = hdr[kHdrBase + k];
@@ -346,18 +347,22 @@ __global__ void __launch_bounds__(kPlanBlock, BKD_PLAN_OCC) plan_emit_kernel(con
         const uint32_t sb = cursor[slot_col(pg)] + ex_ps;
         const bool has_head = p.jh != pg.jc;
         const uint32_t hpos = has_head ? atomicAdd(&cursor[p.jh], 1u) : 0u;
-        const bool overflow = ((uint64_t)rs + p.full > capacity) || (has_head && (uint64_t)hpos >= capacity) ||
-                              (p.ps && (uint64_t)sb + p.ps > capacity);
+        const bool overflow = ((uint64_t)rs + p.full > capacity) || (has_head && (uint64_t)hpos >= capacity);
         const uint32_t seed = seeds ? seeds[i] : seed_all;
-        if (rep == 0u) pslot[i] = overflow ? kDirect : (p.ps ? sb : kNoSlot);
+        // a chunk's partial goes to partials[its list position]: a wave's groups hold consecutive
+        // positions, so their partials are one coalesced write (entry-ordered slots made every
+        // partial a lone 4-byte write). pslot: the full run's first position, or the head's
+        // position when the entry has no full chunk; hslot: the head's when it has both
+        (void)sb;
+        if (rep == 0u) pslot[i] = overflow ? kDirect : (p.ps ? (p.full ? rs : hpos) : kNoSlot);
+        if (rep == 0u && p.ps && p.full && has_head) hslot[i] = hpos;
         if (rep == 0u && has_head && (uint64_t)hpos < capacity)
-            descs[hpos] = overflow ? skip_desc() : chunk_desc(p, p.m - 1u, seed, (uint32_t)i, sb, pg);
+            descs[hpos] = overflow ? skip_desc() : chunk_desc(p, p.m - 1u, seed, (uint32_t)i, hpos, pg);
         st_ae[threadIdx.x] = p.ae;
         st_s[threadIdx.x] = p.s;
         st_m[threadIdx.x] = p.m;
         st_flags[threadIdx.x] = p.pad | (p.ps == 0u ? 0x100u : 0u) | (overflow ? 0x200u : 0u);
         st_seed[threadIdx.x] = seed;
-        st_slot[threadIdx.x] = sb;
     }
     __syncthreads();
     // replicas split the full chunks only when nothing can overflow (total <= capacity): head
@@ -387,7 +392,7 @@ __global__ void __launch_bounds__(kPlanBlock, BKD_PLAN_OCC) plan_emit_kernel(con
             if (pos < capacity) descs[pos] = skip_desc();
         } else {
             descs[pos] = chunk_desc_of(st_ae[t], st_s[t], st_m[t], fl & 0xFFu, (fl & 0x100u) != 0u, c, st_seed[t],
-                                       (uint32_t)((uint64_t)eb * kPlanBlock + t), st_slot[t], pg);
+                                       (uint32_t)((uint64_t)eb * kPlanBlock + t), (uint32_t)pos, pg);
         }
     }
     __syncthreads();  // LDS stashes and cursors are rewritten by the next virtual block
@@ -531,8 +536,9 @@ __global__ void __launch_bounds__(1024, BKD_PLAN_OCC) plan_combine_kernel(
     const uint32_t* __restrict__ seeds, uint32_t seed_all, uint64_t size, uint64_t n, PlanGeo pg,
     const uint32_t* __restrict__ xtab, uint32_t xval,
     const uint32_t* __restrict__ btab, const uint32_t* __restrict__ xinv, uint32_t poly,
-    const uint32_t* __restrict__ pslot, const uint32_t* __restrict__ partials, uint32_t* __restrict__ out,
-    uint32_t* __restrict__ err, uint32_t reps, const uint32_t* __restrict__ blive, uint32_t nblk, PlanRun run) {
+    const uint32_t* __restrict__ pslot, const uint32_t* __restrict__ hslot, const uint32_t* __restrict__ partials,
+    uint32_t* __restrict__ out, uint32_t* __restrict__ err, uint32_t reps, const uint32_t* __restrict__ blive,
+    uint32_t nblk, PlanRun run) {
     // `reps` virtual blocks per 1024-entry block (as plan_emit_kernel): each replica lists the
     // block's entries of > kCombineSerial chunks and combines its share of them; replica 0 does the
     // rest (invalid and serial entries are idempotent writes, cheap, and left to every replica).
@@ -570,8 +576,10 @@ __global__ void __launch_bounds__(1024, BKD_PLAN_OCC) plan_combine_kernel(
                 is_big = 1u;
                 if (reps == 1u) big[atomicAdd(&nbig, 1u)] = (uint32_t)threadIdx.x;
             } else if (rep == 0u) {
-                // partials in batches of 8 independent loads, then Horner from the head
-                uint32_t reg = partials[slot + p.m - 1u];
+                // partials in batches of 8 independent loads, then Horner from the head (chunk m - 1:
+                // at hslot when it is a separate head beside full chunks, else in the full run)
+                const bool sep = p.jh != pg.jc && p.full != 0u;
+                uint32_t reg = partials[sep ? hslot[i] : slot + p.m - 1u];
                 for (int c0 = (int)p.m - 2; c0 >= 0; c0 -= 8) {
                     uint32_t pv[8];
 #pragma unroll
@@ -604,12 +612,13 @@ __global__ void __launch_bounds__(1024, BKD_PLAN_OCC) plan_combine_kernel(
         const uint64_t e = (uint64_t)eb * blockDim.x + big[k];
         const EntryPlan p = plan_entry(offsets[e], lengths[e], size, pg);
         if (p.m > kCombineWave) continue;  // wave-uniform
-        const uint32_t sl = pslot[e];
+        const uint32_t sl = pslot[e], hs = p.jh != pg.jc ? hslot[e] : sl + p.m - 1u;  // m > 64: full chunks exist
         const uint32_t per = (p.m + 63u) >> 6;
         const uint32_t lo = lane * per;
         const uint32_t hi = lo + per < p.m ? lo + per : p.m;
         uint32_t r = 0u;
-        for (int c = (int)hi - 1; c >= (int)lo; --c) r = mul_x(X, r) ^ partials[sl + (uint32_t)c];
+        for (int c = (int)hi - 1; c >= (int)lo; --c)
+            r = mul_x(X, r) ^ partials[(uint32_t)c + 1u == p.m ? hs : sl + (uint32_t)c];
         if (lo < hi && lo) r = gf_mul_bits(gf_pow_bits(xval, lo, poly), r, poly);
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) r ^= (uint32_t)__shfl_xor((int)r, d);
@@ -620,12 +629,13 @@ __global__ void __launch_bounds__(1024, BKD_PLAN_OCC) plan_combine_kernel(
         const uint64_t e = (uint64_t)eb * blockDim.x + big[k];
         const EntryPlan p = plan_entry(offsets[e], lengths[e], size, pg);
         if (p.m <= kCombineWave) continue;  // block-uniform
-        const uint32_t sl = pslot[e];
+        const uint32_t sl = pslot[e], hs = p.jh != pg.jc ? hslot[e] : sl + p.m - 1u;
         const uint32_t per = (p.m + blockDim.x - 1u) / blockDim.x;
         const uint32_t lo = threadIdx.x * per;
         const uint32_t hi = lo + per < p.m ? lo + per : p.m;
         uint32_t r = 0u;
-        for (int c = (int)hi - 1; c >= (int)lo; --c) r = mul_x(X, r) ^ partials[sl + (uint32_t)c];
+        for (int c = (int)hi - 1; c >= (int)lo; --c)
+            r = mul_x(X, r) ^ partials[(uint32_t)c + 1u == p.m ? hs : sl + (uint32_t)c];
         if (lo < hi && lo) r = gf_mul_bits(gf_pow_bits(xval, lo, poly), r, poly);
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) r ^= (uint32_t)__shfl_xor((int)r, d);
