@@ -335,16 +335,14 @@ __global__ void __launch_bounds__(kPlanBlock, BKD_PLAN_OCC) plan_emit_kernel(con
     p.kind = 1;
     if (i < n) p = plan_entry(offsets[i], lengths[i], size, pg);
     const bool chunked = i < n && p.kind == 0;
-    uint32_t t_full, t_ps;
+    uint32_t t_full;
     const uint32_t ex_full = block_excl_scan(chunked ? p.full : 0u, wsum, t_full);
-    const uint32_t ex_ps = block_excl_scan(chunked ? p.ps : 0u, wsum, t_ps);
     const uint32_t run0 = cursor[pg.jc];  // the block's first full-bin position (heads never move it)
     exf[threadIdx.x] = ex_full;
     if (threadIdx.x == 0) exf[kPlanBlock] = t_full;
     if (rep == 0u && i < n && !chunked) pslot[i] = p.kind == 3u ? kSmall : kSerial;
     if (chunked) {
         const uint32_t rs = run0 + ex_full;
-        const uint32_t sb = cursor[slot_col(pg)] + ex_ps;
         const bool has_head = p.jh != pg.jc;
         const uint32_t hpos = has_head ? atomicAdd(&cursor[p.jh], 1u) : 0u;
         const bool overflow = ((uint64_t)rs + p.full > capacity) || (has_head && (uint64_t)hpos >= capacity);
@@ -353,7 +351,6 @@ __global__ void __launch_bounds__(kPlanBlock, BKD_PLAN_OCC) plan_emit_kernel(con
         // positions, so their partials are one coalesced write (entry-ordered slots made every
         // partial a lone 4-byte write). pslot: the full run's first position, or the head's
         // position when the entry has no full chunk; hslot: the head's when it has both
-        (void)sb;
         if (rep == 0u) pslot[i] = overflow ? kDirect : (p.ps ? (p.full ? rs : hpos) : kNoSlot);
         if (rep == 0u && p.ps && p.full && has_head) hslot[i] = hpos;
         if (rep == 0u && has_head && (uint64_t)hpos < capacity)
