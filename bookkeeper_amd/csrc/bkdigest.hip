@@ -389,7 +389,7 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     // non-overlapping entries need at most sum(ceil((len + 127) / CH)) <= n + (size + 127 n) / CH chunks
     const uint64_t capacity = std::min<uint64_t>(n + (size + 128u * n) / pg.ch + 16, 0xFFFFFFF0ull);
     const uint32_t nb = (uint32_t)((n + bkd::kPlanBlock - 1) / bkd::kPlanBlock);
-    const uint32_t ncols = pg.nbins + 1u;
+    const uint32_t ncols = bkd::plan_ncols(pg);
     Carver cv;
     const size_t o_blk = cv.take((size_t)nb * ncols * 4), o_live = cv.take((size_t)nb * 4),
                  o_bok = cv.take((size_t)nb * 4),

@@ -55,7 +55,6 @@ constexpr uint32_t kSerialMax = 64u;
 
 // hdr words
 constexpr int kHdrTotal = 0;  // all chunks
-constexpr int kHdrSlots = 1;  // partial slots
 constexpr int kHdrWork = 2;   // descriptors to process = min(total, capacity)
 constexpr int kHdrBase = 4;   // kHdrBase + col: total of column col (plan_scan)
 constexpr int kHdrWords = kHdrBase + kMaxJC + 2;
@@ -159,9 +158,9 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
     return r;
 }
 
-// columns: bins 0 .. nbins-1 (chunk counts by step count; bin JC = full bucket), then slots.
-__device__ __forceinline__ uint32_t plan_ncols(const PlanGeo& pg) { return pg.nbins + 1u; }
-__device__ __forceinline__ uint32_t slot_col(const PlanGeo& pg) { return pg.nbins; }
+// columns: bins 0 .. nbins-1 (chunk counts by step count; bin JC = full bucket). (Partials need no
+// column of their own: each chunk's partial sits at its own list position.)
+__host__ __device__ __forceinline__ uint32_t plan_ncols(const PlanGeo& pg) { return pg.nbins; }
 
 // Per-block column counts (plan_scan_kernel turns them into per-block offsets and totals).
 // blive[b]: entries of block b that the plan itself handles (not the short-entry class); emit and
@@ -184,7 +183,7 @@ __global__ void __launch_bounds__(kPlanBlock) plan_count_kernel(const uint64_t* 
     }
     __syncthreads();
     const uint64_t i = (uint64_t)eb * kPlanBlock + threadIdx.x;
-    uint32_t full = 0u, ps = 0u, mine = 0u;
+    uint32_t full = 0u, mine = 0u;
     bool ok = true;  // length within the band of the reference (PlanRun::in_band)
     if (i < n) {
         const uint32_t l = lengths[i];
@@ -195,7 +194,6 @@ __global__ void __launch_bounds__(kPlanBlock) plan_count_kernel(const uint64_t* 
             if (p.kind == 0) {
                 if (p.jh != pg.jc) atomicAdd(&col[p.jh], 1u);
                 full = p.full;
-                ps = p.ps;
             }
         }
     }
@@ -203,13 +201,11 @@ __global__ void __launch_bounds__(kPlanBlock) plan_count_kernel(const uint64_t* 
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         full += (uint32_t)__shfl_xor((int)full, d);
-        ps += (uint32_t)__shfl_xor((int)ps, d);
         mine += (uint32_t)__shfl_xor((int)mine, d);
     }
     const bool wave_ok = __all(ok);
     if ((threadIdx.x & 63) == 0) {
         if (full) atomicAdd(&col[pg.jc], full);
-        if (ps) atomicAdd(&col[slot_col(pg)], ps);
         if (mine) atomicAdd(&live, mine);
         if (!wave_ok) bad = 1u;  // (a per-wave min/max with global atomics cost +330 us per 1 M entries)
     }
@@ -314,12 +310,9 @@ __global__ void __launch_bounds__(kPlanBlock, BKD_PLAN_OCC) plan_emit_kernel(con
             bin0[j] = acc;
             acc += t;
         }
-        const uint32_t slots = bin0[slot_col(pg)];
-        bin0[slot_col(pg)] = 0;
         s_total = acc;
         if (blockIdx.x == 0) {  // the block that plans entry block 0, replica 0
             hdr[kHdrTotal] = acc;
-            hdr[kHdrSlots] = slots;
             hdr[kHdrWork] = (uint32_t)((uint64_t)acc < capacity ? acc : capacity);
         }
     }
