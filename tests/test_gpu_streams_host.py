@@ -342,3 +342,48 @@ def test_plan_serial_entries(gpu, serial):
         ck.set_plan_mode(0)
         ck.set_plan_small(192)
         ck.set_plan_serial(16)
+
+
+def test_plan_short_entries_among_long(gpu):
+    """Short entries among long ones (the base buffer holds > 1 KiB per entry, so no short-entry
+    launch): they are one-step chunks of the plan. Mixed lengths (0..192 and 3..9 KiB, shuffled),
+    seeded, both algorithms; an out-of-range short entry is reported; a batch of nearly equal short
+    entries spread over the large buffer takes the uniform route with the same digests."""
+    import torch
+    rng = np.random.default_rng(71)
+    short = rng.integers(0, 193, 3000)
+    long_ = rng.integers(3000, 9000, 1500)
+    lens = np.concatenate([short, long_, np.arange(0, 193)]).astype(np.int64)
+    rng.shuffle(lens)
+    offs = np.concatenate([[11], 11 + np.cumsum(lens[:-1] + rng.integers(0, 40, lens.size - 1))]).astype(np.int64)
+    size = int(offs[-1] + lens[-1]) + 513
+    assert size > 1024 * lens.size  # no short-entry launch
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    seeds = rng.integers(0, 2**32, lens.size, dtype=np.uint64).astype(np.uint32)
+    base = _dev(torch, host, gpu)
+    d_seeds = _dev(torch, seeds.view(np.int32), gpu)
+    ck.set_plan_mode(2)
+    try:
+        for algo in (0, 1):
+            want = oracle.batch(algo, host, offs.astype(np.uint64), lens.astype(np.uint32), seeds=seeds)
+            out = ck.crc_batch(algo, base, _dev(torch, offs, gpu), _dev(torch, lens.astype(np.int32), gpu),
+                               seeds=d_seeds, sync_check=True)
+            got = out.cpu().numpy().view(np.uint32)
+            bad = np.nonzero(got != want)[0]
+            assert bad.size == 0, (algo, lens[bad[:5]])
+        k = int(np.nonzero((lens > 20) & (lens < 150))[0][0])
+        bad_o = offs.copy()
+        bad_o[k] = size - 5
+        with pytest.raises(BkdError) as e:
+            ck.crc_batch(0, base, _dev(torch, bad_o, gpu), _dev(torch, lens.astype(np.int32), gpu), seeds=d_seeds,
+                         sync_check=True)
+        assert e.value.code == -4
+        # nearly equal short entries spread over the large buffer: uniform route
+        n2 = 5000
+        l2 = rng.integers(100, 110, n2).astype(np.int64)
+        o2 = np.sort(rng.choice(size - 200, n2, replace=False)).astype(np.int64)
+        want = oracle.batch(0, host, o2.astype(np.uint64), l2.astype(np.uint32))
+        out = ck.crc_batch(0, base, _dev(torch, o2, gpu), _dev(torch, l2.astype(np.int32), gpu), sync_check=True)
+        assert (out.cpu().numpy().view(np.uint32) == want).all()
+    finally:
+        ck.set_plan_mode(0)
