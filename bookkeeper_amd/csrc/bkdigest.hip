@@ -402,8 +402,8 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     uint32_t* err = nullptr;
     uint32_t* run_word = nullptr;
     uint32_t* uni = nullptr;
-    // without a short class (mean entry > 1 KiB), lengths within an eighth of each other skip the
-    // chunks: the chunk kernel computes them whole, as the direct kernel would (PlanRun::uniform,
+    // without a short class (mean entry > 1 KiB), lengths all within 1/16 + 64 B of the first
+    // entry's skip the chunks: the chunk kernel computes them whole, as the direct kernel would (PlanRun::uniform,
     // decided on the device: plan_count's per-block ballots, reduced by plan_scan). Only where the
     // direct kernel would use the plan's lane count.
 #ifndef BKD_DIRECT_GATE

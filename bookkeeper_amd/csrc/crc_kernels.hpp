@@ -772,22 +772,14 @@ __device__ __forceinline__ ChunkGeo chunk_geo(const PlanDesc& d, int g) {
 }
 
 // Loads of step 0 and steps 1..PF of chunk c (addresses past the chunk clamp to a valid block).
-#ifndef BKD_PF_SKIP
-#define BKD_PF_SKIP 0
-#endif
 template <int G, int PF, bool NT>
 __device__ __forceinline__ void chunk_prefetch(const uint8_t* __restrict__ base, const ChunkGeo& c, u32x4& W0,
                                                u32x4 (&A)[PF]) {
     W0 = ld16<NT>(base + c.la0);
 #pragma unroll
     for (int k = 0; k < PF; ++k) {
-        if constexpr (BKD_PF_SKIP) {
-            // steps past the chunk are not loaded at all (no duplicate requests for short chunks)
-            if ((uint32_t)(k + 1) < c.J) A[k] = ld16<NT>(base + c.a + (int64_t)(k + 1) * Geo<G>::kStep);
-        } else {
-            const int64_t addr = (uint32_t)(k + 1) < c.J ? c.a + (int64_t)(k + 1) * Geo<G>::kStep : c.la0;
-            A[k] = ld16<NT>(base + addr);
-        }
+        const int64_t addr = (uint32_t)(k + 1) < c.J ? c.a + (int64_t)(k + 1) * Geo<G>::kStep : c.la0;
+        A[k] = ld16<NT>(base + addr);
     }
 }
 
@@ -958,84 +950,6 @@ __device__ __forceinline__ void plan_chunks_loop(const uint32_t* lds, uint32_t l
 #undef BKD_CHUNK_HALF
 }
 
-// Per-block work queue over the sorted chunk list (BKD_SCHED=1): block b owns positions b, b + NB,
-// b + 2NB, ... (every block the same mix of long and short chunks); its waves take rounds of one
-// chunk per group alternately from the front (longest) and the back (shortest) of that sub-list
-// through one 64-bit LDS atomic {front, back}, so short chunks (finish- and latency-bound) run
-// beside long ones (bandwidth-bound) instead of all at the end.
-template <int G, int PF, bool NT>
-__device__ __forceinline__ void plan_chunks_queue(const uint32_t* lds, uint32_t lanereg, int g,
-                                                  const uint8_t* __restrict__ base, const PlanDesc* __restrict__ descs,
-                                                  uint32_t* __restrict__ out, uint32_t* __restrict__ partials,
-                                                  unsigned long long* q) {
-    constexpr uint32_t kGPW = 64u / (uint32_t)G;  // groups per wave
-    const uint32_t NB = gridDim.x, b = blockIdx.x;
-    const int lane = threadIdx.x & 63;
-    const int32_t gi = lane / G;
-    bool front = ((threadIdx.x >> 6) & 1u) == 0u;
-    bool exhausted = false;
-    auto fetch = [&](int32_t k) -> PlanDesc {
-        if (k < 0) return PlanDesc{0ull, 0u, 0u};
-        return descs[(uint64_t)b + (uint64_t)k * NB];
-    };
-    auto grab = [&]() -> int32_t {
-        if (exhausted) return -1;
-        unsigned long long old = 0ull;
-        const unsigned long long inc = front ? (unsigned long long)kGPW : ((unsigned long long)(0u - kGPW) << 32);
-        if (lane == 0) old = atomicAdd(q, inc);
-        const int32_t F = (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)old);
-        const int32_t B = (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)(old >> 32));
-        int32_t k;
-        if (front) k = F + gi < B ? F + gi : -1;
-        else k = B - 1 - gi >= F ? B - 1 - gi : -1;
-        if (F >= B) exhausted = true;  // wave-uniform; every later grab is empty too
-        front = !front;
-        return k;
-    };
-    auto pf_geo = [&](const ChunkGeo& nx, const ChunkGeo& cur) -> const ChunkGeo& { return nx.len ? nx : cur; };
-    auto emit = [&](const ChunkGeo& c, uint32_t v) {
-        if (g == 0 && c.len) {
-            if (c.dst & kPlanFinal) out[c.dst & ~kPlanFinal] = ~v;
-            else partials[c.dst] = v;
-        }
-    };
-    u32x4 W0x, Ax[PF], Bx[PF], W0y, Ay[PF], By[PF];
-    ChunkGeo cur = chunk_geo<G>(fetch(grab()), g);
-    PlanDesc dn = fetch(grab());
-    ChunkGeo safe = cur;
-    if (!cur.len) safe.la0 = safe.a = 0, safe.J = 1;  // hole first: prefetch base[0..16)
-    chunk_prefetch<G, PF, NT>(base, cur.len ? cur : safe, W0x, Ax);
-    for (;;) {
-        {  // current chunk in set X, prefetch into Y
-            const PlanDesc dnn = fetch(grab());
-            const ChunkGeo nx = chunk_geo<G>(dn, g);
-            const ChunkGeo& pg = pf_geo(nx, cur.len ? cur : safe);
-            const uint32_t v = cur.len ? chunk_fold<G, PF, NT>(lds, lanereg, g, base, cur, W0x, Ax, Bx, pg, W0y, Ay)
-                                       : (chunk_prefetch<G, PF, NT>(base, pg, W0y, Ay), 0u);
-            emit(cur, v);
-            if (exhausted && !__any(nx.len != 0u || (uint32_t)(dnn.s_len >> 48) != 0u)) break;
-            if (cur.len) safe = cur;
-            cur = nx;
-            dn = dnn;
-        }
-        {  // current chunk in set Y, prefetch into X
-            const PlanDesc dnn = fetch(grab());
-            const ChunkGeo nx = chunk_geo<G>(dn, g);
-            const ChunkGeo& pg = pf_geo(nx, cur.len ? cur : safe);
-            const uint32_t v = cur.len ? chunk_fold<G, PF, NT>(lds, lanereg, g, base, cur, W0y, Ay, By, pg, W0x, Ax)
-                                       : (chunk_prefetch<G, PF, NT>(base, pg, W0x, Ax), 0u);
-            emit(cur, v);
-            if (exhausted && !__any(nx.len != 0u || (uint32_t)(dnn.s_len >> 48) != 0u)) break;
-            if (cur.len) safe = cur;
-            cur = nx;
-            dn = dnn;
-        }
-    }
-}
-
-#ifndef BKD_SCHED
-#define BKD_SCHED 0
-#endif
 
 // Chunk kernel of the ragged-batch plan: one chunk per group, grid stride over the descriptor
 // list (sorted by step count, plan_kernels.hpp). Descriptors are read two rounds ahead and each
@@ -1053,14 +967,11 @@ __global__ void __launch_bounds__(kBlock) crc_plan_chunks_kernel(const uint8_t* 
     using Gm = Geo<G>;
     if (!run.plan_entries()) return;  // only short entries
     __shared__ __attribute__((aligned(16))) uint32_t lds[Gm::kLdsWords];
-    __shared__ unsigned long long queue;  // {front, back} of this block's sub-list (BKD_SCHED)
-    // lengths within an eighth of each other: no chunks, every entry whole as in the direct kernel
+    // near-uniform lengths (PlanRun::uniform): no chunks, every entry whole as in the direct kernel
     ov.all = run.uniform();
     const uint64_t n = ov.all ? 0u : *count;
     const uint64_t nov = ov.count();
     if (n == 0 && nov == 0) return;  // every entry was short or serial: no table staging
-    if (BKD_SCHED && threadIdx.x == 0)
-        queue = (unsigned long long)(n > blockIdx.x ? (n - blockIdx.x + gridDim.x - 1) / gridDim.x : 0u) << 32;
     stage_tables<G>(lds, tables);
 
     const int lane = threadIdx.x & 63;
@@ -1068,11 +979,7 @@ __global__ void __launch_bounds__(kBlock) crc_plan_chunks_kernel(const uint8_t* 
     const uint32_t lanereg = ((uint32_t)(lane & 31) << 2) | (1u << 16);
     const uint64_t ngroups = (uint64_t)gridDim.x * (kBlock / G);
     const uint64_t gid = (uint64_t)blockIdx.x * (kBlock / G) + (uint64_t)(threadIdx.x / G);
-    if constexpr (BKD_SCHED != 0) {
-        if (n) plan_chunks_queue<G, PF, NT>(lds, lanereg, g, base, descs, out, partials, &queue);
-    } else {
-        if (gid < n) plan_chunks_loop<G, PF, NT>(lds, lanereg, g, base, descs, n, gid, ngroups, out, partials);
-    }
+    if (gid < n) plan_chunks_loop<G, PF, NT>(lds, lanereg, g, base, descs, n, gid, ngroups, out, partials);
     if (nov) groups_loop<G, PF, NT>(lds, lanereg, g, base, ov, nov, gid, ngroups, err);
 }
 
