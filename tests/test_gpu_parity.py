@@ -635,3 +635,49 @@ def test_crc_batch_segments(gpu):
         for i in range(n):
             cat = b"".join(data[offs[k]:offs[k] + lens[k]].tobytes() for k in range(seg_first[i], seg_first[i + 1]))
             assert got[i] == oracle.resume(algo, int(seeds[i]), cat), (algo, i)
+
+
+@pytest.mark.parametrize("trial", range(6))
+def test_plan_random_ragged_batches(gpu, trial):
+    """Randomised ragged batches through the automatic route: per trial a fresh mix of length
+    distributions (tiny, Zipf-like, near-uniform, huge), packed or scattered or overlapping
+    offsets, a base pointer misaligned by 0..127 bytes, per-entry or shared seeds, CRC32C and CRC32
+    — every digest against the oracle. Covers the plan's descriptor windows, position-indexed
+    partials, separate heads, the uniformity gate and the short-entry launch together."""
+    import torch
+    rng = np.random.default_rng(9000 + trial)
+    n = int(rng.integers(2000, 12000))
+    kind = trial % 3
+    if kind == 0:
+        lens = np.minimum(64 * rng.zipf(1.1, n), 65536) - rng.integers(0, 64, n)
+    elif kind == 1:
+        lens = rng.integers(0, 300, n)
+        lens[rng.integers(0, n, 50)] = rng.integers(4096, 200000, 50)
+    else:
+        lens = rng.integers(3900, 4300, n)
+        lens[rng.integers(0, n, 5)] = rng.integers(0, 100, 5)
+    lens = np.maximum(lens, 0).astype(np.int64)
+    layout = int(rng.integers(0, 3))
+    if layout == 0:  # packed
+        offs = np.concatenate([[0], np.cumsum(lens[:-1])])
+    elif layout == 1:  # gaps
+        offs = np.concatenate([[0], np.cumsum(lens[:-1] + rng.integers(0, 300, n - 1))])
+    else:  # shuffled, some overlapping
+        offs = np.concatenate([[0], np.cumsum(lens[:-1])])
+        rng.shuffle(offs)
+        offs = np.maximum(offs - rng.integers(0, 64, n), 0)
+    size = int((offs + lens).max()) + int(rng.integers(1, 4096))
+    mis = int(rng.integers(0, 128))
+    data = oracle.fill_splitmix64(size + 128, 700 + trial)
+    big = _dev_bytes(torch, data, gpu)
+    base = big[mis:mis + size]
+    host = data[mis:mis + size]
+    seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32) if trial % 2 else None
+    d_offs = torch.from_numpy(offs.astype(np.int64)).to(gpu)
+    d_lens = torch.from_numpy(lens.astype(np.int32)).to(gpu)
+    d_seeds = torch.from_numpy(seeds.view(np.int32)).to(gpu) if seeds is not None else None
+    for algo in (ck.CRC32C, ck.CRC32):
+        want = oracle.batch(algo, host, offs.astype(np.uint64), lens.astype(np.uint32), seeds=seeds)
+        got = ck.crc_batch(algo, base, d_offs, d_lens, seeds=d_seeds, sync_check=True).cpu().numpy().view(np.uint32)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (trial, algo, bad.size, lens[bad[:5]], offs[bad[:5]])
