@@ -466,7 +466,7 @@ int indexed_batch(DeviceState& ds, int algo, const uint8_t* base, uint64_t size,
                   const uint32_t* lengths, uint64_t n, const uint32_t* seeds, uint32_t seed_all, uint32_t* out,
                   hipStream_t st) {
     const int mode = g_plan_mode.load();
-    // plan descriptors hold 41-bit offsets (PlanDesc): larger buffers take the direct kernel
+    // plan descriptors hold a biased 41-bit window start (PlanDesc): buffers >= 1 TiB take the direct kernel
     const bool direct = mode == 1 || (mode == 0 && size <= kDirectMaxBytes) || size >= bkd::kPlanMaxSize;
     if (!direct) return launch_plan(ds, algo, base, size, offsets, lengths, n, seeds, seed_all, out, st);
     uint32_t* err = nullptr;
