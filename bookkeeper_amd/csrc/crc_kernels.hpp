@@ -799,10 +799,16 @@ __device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lan
     else w = u32x4{0u, 0u, 0u, 0u};
     const uint32_t r0 = c.r0;
     if (d0 > -4 && d0 < 16) {
-        w.x ^= place_seed(r0, d0);
-        w.y ^= place_seed(r0, d0 - 4);
-        w.z ^= place_seed(r0, d0 - 8);
-        w.w ^= place_seed(r0, d0 - 12);
+        // the seed image is r0 << 8*d0 across the 16-byte block: dword k = (r0:0 >> (32 + 32k - 8*d0))
+        const uint64_t R = (uint64_t)r0 << 32;
+        auto part = [&](int k) -> uint32_t {
+            const int32_t t = 32 + 32 * k - 8 * d0;
+            return (t > 0 && t < 64) ? (uint32_t)(R >> t) : 0u;
+        };
+        w.x ^= part(0);
+        w.y ^= part(1);
+        w.z ^= part(2);
+        w.w ^= part(3);
     }
     uint32_t fx = 0u;
     if (d0 > Gm::kStep - 4) fx = place_seed(r0, d0 - Gm::kStep);
