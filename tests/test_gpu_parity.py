@@ -681,3 +681,46 @@ def test_plan_random_ragged_batches(gpu, trial):
         got = ck.crc_batch(algo, base, d_offs, d_lens, seeds=d_seeds, sync_check=True).cpu().numpy().view(np.uint32)
         bad = np.nonzero(got != want)[0]
         assert bad.size == 0, (trial, algo, bad.size, lens[bad[:5]], offs[bad[:5]])
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_offsets_beyond_4gib(gpu, mode):
+    """64-bit addressing: indexed entries just below, across and above the 4 GiB mark of one base
+    buffer (automatic route, one entry per group, chunked plan), and a uniform batch whose stride
+    carries entries past 4 GiB — each digest against the oracle over a host copy of its window."""
+    import torch
+    ck.set_plan_mode(mode)
+    four = 1 << 32
+    size = four + (3 << 20)
+    base = torch.empty(size, dtype=torch.uint8, device=gpu)
+    ck.fill_splitmix64(base, 4242)
+    w0 = four - (1 << 20)
+    win = base[w0:].cpu().numpy()  # every indexed entry lies in [4 GiB - 1 MiB, size)
+    rng = np.random.default_rng(4 + mode)
+    n = 3000
+    lens = rng.integers(0, 70000, n)
+    lens[:300] = rng.integers(0, 300, 300)
+    offs = rng.integers(w0, size - 70000, n).astype(np.int64)
+    offs[300:340] = four - rng.integers(1, 60000, 40)  # entries straddling 2^32
+    lens[300:340] = four - offs[300:340] + rng.integers(1, 5000, 40)
+    offs[340] = size - 17
+    lens[340] = 17  # the buffer's last bytes
+    seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    d_offs = torch.from_numpy(offs).to(gpu)
+    d_lens = torch.from_numpy(lens.astype(np.int32)).to(gpu)
+    d_seeds = torch.from_numpy(seeds.view(np.int32)).to(gpu)
+    for algo in (ck.CRC32C, ck.CRC32):
+        got = ck.crc_batch(algo, base, d_offs, d_lens, seeds=d_seeds, sync_check=True).cpu().numpy().view(np.uint32)
+        want = oracle.batch(algo, win, (offs - w0).astype(np.uint64), lens.astype(np.uint32), seeds=seeds)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (mode, algo, bad.size, offs[bad[:5]], lens[bad[:5]])
+    # uniform: entry i at i * stride; the last entries start past 4 GiB
+    stride, elen = (1 << 20) + 4160, 4096 + 37
+    nu = (size - elen) // stride + 1
+    got = ck.crc_batch_uniform(ck.CRC32C, base, elen, nu, stride=stride).cpu().numpy().view(np.uint32)
+    hi = [i for i in range(nu) if i * stride + elen > four - (1 << 20)]
+    assert hi and hi[-1] * stride > four
+    for i in hi + [0, 1]:
+        o = i * stride
+        blob = base[o:o + elen].cpu().numpy()
+        assert got[i] == oracle.resume(ck.CRC32C, 0, blob.tobytes()), i
