@@ -57,6 +57,7 @@ PROTOTYPES = {
     "bkd_crc_batch": (_int, [_int, _vp, _u64, _vp, _vp, _u64, _vp, _u32, _vp, _vp]),
     "bkd_crc_batch_segments": (_int, [_int, _vp, _u64, _vp, _vp, _u64, _vp, _u64, _vp, _u32, _vp, _vp]),
     "bkd_stream_sync": (_int, [_vp]),
+    "bkd_stream_release": (_int, [_vp]),
     "bkd_crc_batch_host": (_int, [_int, _vp, _u64, _vp, _vp, _u64, _vp, _u32, _vp]),
     "bkd_resume": (_int, [_int, _u32, _vp, _u64, _c.POINTER(_u32)]),
     "bkd_resume_host": (_int, [_int, _u32, _vp, _u64, _c.POINTER(_u32)]),

@@ -31,7 +31,7 @@ from . import _native
 from ._native import CRC32, CRC32C, check, lib
 
 __all__ = ["CRC32C", "CRC32", "GpuIntHash", "Crc32cIntChecksum", "crc_batch", "crc_batch_uniform",
-           "crc_batch_segments", "crc_batch_host", "cpu_resume", "set_cpu_route_max", "to_java_int"]
+           "crc_batch_segments", "crc_batch_host", "release_stream", "cpu_resume", "set_cpu_route_max", "to_java_int"]
 
 
 def to_java_int(v: int) -> int:
@@ -278,6 +278,19 @@ def fill_splitmix64(buf, seed: int, first_word: int = 0, stream=None) -> None:
     with _on_device(buf):
         check(lib().bkd_fill_splitmix64(_dev_ptr(buf, "buf"), nbytes, seed & (2**64 - 1), first_word,
                                         _stream_ptr(stream, buf)))
+
+
+def release_stream(stream) -> None:
+    """Waits for `stream` and frees the library's scratch for it (bkd_stream_release): call before a
+    stream that ran indexed batches is dropped. Raises BKD_ERR_BOUNDS as a sync would."""
+    ptr = _stream_ptr(stream)
+    sdev = getattr(stream, "device", None)
+    if sdev is not None:
+        import torch
+        with torch.cuda.device(sdev):
+            check(lib().bkd_stream_release(ptr))
+    else:
+        check(lib().bkd_stream_release(ptr))
 
 
 def cpu_resume(algo: int, current: int, buffer) -> int:

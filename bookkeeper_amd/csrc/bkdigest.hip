@@ -899,6 +899,10 @@ uint64_t cpu_route_max() {
     return bkd::host::has_wide_fold() ? (64ull << 20) : (4ull << 20);
 }
 
+// Per-call resumes longer than this run as consecutive pieces, each resuming from the last
+// (entry lengths are 32-bit in the batch kernels).
+constexpr uint64_t kResumePiece = 1ull << 31;
+
 int cpu_resume(int algo, uint32_t current, const void* p, uint64_t len, uint32_t* out) {
     *out = ~bkd::host::crc_raw(algo, ~current, (const uint8_t*)p, (size_t)len);
     return BKD_OK;
@@ -1096,6 +1100,42 @@ int bkd_stream_sync(void* stream) {
     return BKD_OK;
 }
 
+int bkd_stream_release(void* stream) {
+    const hipStream_t st = (hipStream_t)stream;
+    DeviceScope scope;
+    DeviceState* ds = nullptr;
+    int rc = enter(st, scope, &ds);
+    if (rc) return rc;
+    std::unique_ptr<StreamScratch> sc;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        auto it = ds->scratch.find(st);
+        if (it == ds->scratch.end()) {
+            BKD_HIP(hipStreamSynchronize(st));
+            return BKD_OK;
+        }
+        sc = std::move(it->second);
+        ds->scratch.erase(it);
+    }
+    int status = BKD_OK;
+    {
+        std::lock_guard<std::recursive_mutex> lk(sc->mu);
+        BKD_HIP(hipStreamSynchronize(st));  // the stream's kernels are done with the scratch
+        if (sc->err) {
+            BKD_HIP(hipMemcpy(sc->h_err, sc->err, sizeof(uint32_t), hipMemcpyDeviceToHost));
+            if (*sc->h_err) status = fail(BKD_ERR_BOUNDS, "an indexed entry exceeded its base buffer (entries skipped, out = 0)");
+        }
+        // stream-ordered allocations go back the way they came
+        for (int k = 0; k < 3; ++k)
+            if (sc->buf[k]) BKD_HIP(hipFreeAsync(sc->buf[k], st));
+        for (uint32_t* w : {sc->err, sc->run, sc->uni})
+            if (w) BKD_HIP(hipFreeAsync(w, st));
+        BKD_HIP(hipStreamSynchronize(st));
+        if (sc->h_err) BKD_HIP(hipHostFree(sc->h_err));
+    }
+    return status;
+}
+
 int bkd_crc_batch_host(int algo, const void* h_base, uint64_t base_size, const uint64_t* h_offsets,
                        const uint32_t* h_lengths, uint64_t n, const uint32_t* h_seeds, uint32_t seed_all,
                        uint32_t* h_out) {
@@ -1139,22 +1179,37 @@ int bkd_resume_host(int algo, uint32_t current, const void* h_ptr, uint64_t len,
     if (!h_ptr) return fail(BKD_ERR_INVALID_ARG, "null buffer");
     if (len <= cpu_route_max() || visible_devices() <= 0)
         return cpu_resume(algo, current, h_ptr, len, out);
-    if (len > 0xFFFFFFFFull) return fail(BKD_ERR_INVALID_ARG, "len > 4 GiB - 1");
-    const uint64_t off = 0;
-    const uint32_t l32 = (uint32_t)len;
-    return bkd_crc_batch_host(algo, h_ptr, len, &off, &l32, 1, nullptr, current, out);
+    // entries are indexed with 32-bit lengths: a longer buffer resumes piece by piece
+    // (Sse42Crc32C.resume takes a long length, Sse42Crc32C.java:105-107)
+    const uint8_t* p = (const uint8_t*)h_ptr;
+    for (uint64_t at = 0; at < len;) {
+        const uint64_t off = 0;
+        const uint32_t l32 = (uint32_t)std::min<uint64_t>(len - at, kResumePiece);
+        const int rc = bkd_crc_batch_host(algo, p + at, l32, &off, &l32, 1, nullptr, current, &current);
+        if (rc) return rc;
+        at += l32;
+    }
+    *out = current;
+    return BKD_OK;
 }
 
 int bkd_resume_device(int algo, uint32_t current, const void* d_ptr, uint64_t len, void* stream, uint32_t* out) {
     if (!valid_algo(algo)) return fail(BKD_ERR_INVALID_ARG, "unknown algorithm");
     if (!out) return fail(BKD_ERR_INVALID_ARG, "null out");
-    if (len > 0xFFFFFFFFull) return fail(BKD_ERR_INVALID_ARG, "len > 4 GiB - 1");
     if (len == 0) {
         *out = current;
         return BKD_OK;
     }
     if (!d_ptr) return fail(BKD_ERR_INVALID_ARG, "null buffer");
-    return resume_device(algo, current, d_ptr, len, (hipStream_t)stream, out);
+    const uint8_t* p = (const uint8_t*)d_ptr;
+    for (uint64_t at = 0; at < len;) {  // 32-bit entry lengths: longer buffers piece by piece
+        const uint64_t l = std::min<uint64_t>(len - at, kResumePiece);
+        const int rc = resume_device(algo, current, p + at, l, (hipStream_t)stream, &current);
+        if (rc) return rc;
+        at += l;
+    }
+    *out = current;
+    return BKD_OK;
 }
 
 int bkd_resume(int algo, uint32_t current, const void* ptr, uint64_t len, uint32_t* out) {

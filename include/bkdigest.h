@@ -117,6 +117,14 @@ BKD_API int bkd_crc_batch_segments(int algo, const void* d_base, uint64_t base_s
  * concurrent callers on other streams neither see nor clear it. */
 BKD_API int bkd_stream_sync(void* stream);
 
+/* Waits for `stream`, then frees the scratch the library keeps for it (plan arena, bounds flag,
+ * run words) and forgets the stream; returns BKD_ERR_BOUNDS as bkd_stream_sync would. Call it
+ * before hipStreamDestroy on a stream that ran indexed batches, with no other call on that stream
+ * in progress; a later call on the same handle starts afresh. The reference has no per-stream state
+ * (its natives are stateless, $CN/cpp/crc32c_sse42_jni.cpp:26-48): this is the lifetime rule a
+ * long-lived caller that creates and drops streams needs so that their scratch does not pile up. */
+BKD_API int bkd_stream_release(void* stream);
+
 /* ---- host-resident batches (the end-to-end path: Netty buffers in, digests out) -------
  * Synchronous. Copies the payload through pinned staging buffers with hipMemcpyAsync
  * (double-buffered H2D -> kernel -> D2H). Same semantics as bkd_crc_batch. */

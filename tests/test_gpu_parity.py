@@ -724,3 +724,29 @@ def test_offsets_beyond_4gib(gpu, mode):
         o = i * stride
         blob = base[o:o + elen].cpu().numpy()
         assert got[i] == oracle.resume(ck.CRC32C, 0, blob.tobytes()), i
+
+
+def test_resume_longer_than_4gib(gpu):
+    """IntHash.resume(int, long address, long length) (Sse42Crc32C.java:105-107) on one buffer past
+    4 GiB: the per-call device and host routes resume piece by piece; both equal one pass of the
+    reference's own crc32c() (CRC32C; the table oracle when that build is absent) and of zlib.crc32
+    (CRC32, = java.util.zip.CRC32) over the whole buffer."""
+    import zlib
+
+    import torch
+    size = (1 << 32) + (3 << 20) + 5
+    base = torch.empty(size, dtype=torch.uint8, device=gpu)
+    ck.fill_splitmix64(base, 777)
+    host = base.cpu().numpy()
+    ref = oracle.ref()
+    for algo, seed in ((ck.CRC32C, 0x1234567), (ck.CRC32, 0x89abcdef)):
+        if algo == ck.CRC32:
+            want = zlib.crc32(host, seed)
+        elif ref is not None:
+            want = int(ref.ref_crc32c(seed, host.ctypes.data, host.size))
+        else:
+            want = oracle.resume(algo, seed, host)
+        want = ck.to_java_int(want)
+        h = ck.GpuIntHash(algo)
+        assert h.resume(seed, base) == want, algo
+        assert h.resume(seed, host) == want, algo  # host buffer > the CPU-route bound: GPU via staging

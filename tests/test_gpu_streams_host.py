@@ -64,6 +64,39 @@ def test_bounds_flag_is_per_stream(gpu):
         assert results["bad"] == ("err", -4), mode
         assert results["good"][0] == "ok", mode
         assert (results["good"][1] == want).all()
+
+
+def test_stream_release_frees_and_restarts(gpu):
+    """bkd_stream_release: waits for the stream, reports its pending bounds flag, frees its scratch;
+    streams created afterwards (whatever handle they get) run indexed batches correctly."""
+    import torch
+    rng = np.random.default_rng(11)
+    size = 4 << 20
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    base = _dev(torch, host, gpu)
+    n = 20000
+    offs = rng.integers(0, size - 70000, n).astype(np.int64)
+    lens = rng.integers(0, 70000, n).astype(np.int32)
+    want = oracle.batch(0, host, offs.astype(np.uint64), lens.astype(np.uint32))
+    d_off, d_len = _dev(torch, offs, gpu), _dev(torch, lens, gpu)
+    bad_off = d_off.clone()
+    bad_off[7] = size - 3
+    torch.cuda.synchronize()  # inputs were made on the current stream; the batches run on others
+    for rnd in range(4):
+        s = torch.cuda.Stream(device=gpu)
+        out = ck.crc_batch(0, base, d_off, d_len, stream=s)
+        if rnd % 2:
+            ck.crc_batch(0, base, bad_off, d_len, stream=s)
+            with pytest.raises(BkdError) as ei:
+                ck.release_stream(s)
+            assert ei.value.code == -4
+        else:
+            ck.release_stream(s)
+        assert (out.cpu().numpy().view(np.uint32) == want).all(), rnd
+        del s
+    ck.release_stream(torch.cuda.current_stream(gpu))  # the current stream's scratch, if it had any
+    out = ck.crc_batch(0, base, d_off, d_len)  # ... is made again by its next call
+    assert (out.cpu().numpy().view(np.uint32) == want).all()
     # the flag was cleared by the sync that reported it
     s = torch.cuda.Stream(device=gpu)
     ck.crc_batch(0, base, _dev(torch, offs, gpu), _dev(torch, lens, gpu), stream=s, sync_check=True)
