@@ -499,7 +499,6 @@ bool is_device_pointer(const void* p) {
 struct HostStage {
     static constexpr size_t kSeg = 64u << 20;
     static constexpr size_t kSegEntries = 1u << 20;
-    std::mutex mu;
     bool ready = false;
     uint8_t* h_pin[2] = {};
     uint8_t* d_buf[2] = {};
@@ -521,13 +520,15 @@ struct HostStage {
     uint8_t* d_aux[2] = {};
     uint8_t* h_frm[2] = {};
     uint8_t* d_frm[2] = {};
+    // (each allocation is made once: a call after a failed init completes the set, nothing leaks)
+    // (each allocation is made once: a call after a failed init completes the set, nothing leaks)
     int init_aux() {
         if (aux_ready) return BKD_OK;
         for (int s = 0; s < 2; ++s) {
-            BKD_HIP(hipHostMalloc((void**)&h_aux[s], kAux, hipHostMallocDefault));
-            BKD_HIP(hipMalloc((void**)&d_aux[s], kAux));
-            BKD_HIP(hipHostMalloc((void**)&h_frm[s], kAux, hipHostMallocDefault));
-            BKD_HIP(hipMalloc((void**)&d_frm[s], kAux));
+            if (!h_aux[s]) BKD_HIP(hipHostMalloc((void**)&h_aux[s], kAux, hipHostMallocDefault));
+            if (!d_aux[s]) BKD_HIP(hipMalloc((void**)&d_aux[s], kAux));
+            if (!h_frm[s]) BKD_HIP(hipHostMalloc((void**)&h_frm[s], kAux, hipHostMallocDefault));
+            if (!d_frm[s]) BKD_HIP(hipMalloc((void**)&d_frm[s], kAux));
         }
         aux_ready = true;
         return BKD_OK;
@@ -535,24 +536,72 @@ struct HostStage {
     int init() {
         if (ready) return BKD_OK;
         for (int s = 0; s < 2; ++s) {
-            BKD_HIP(hipHostMalloc((void**)&h_pin[s], kSeg, hipHostMallocDefault));
-            BKD_HIP(hipMalloc((void**)&d_buf[s], kSeg));
-            BKD_HIP(hipHostMalloc((void**)&h_off[s], kSegEntries * 8, hipHostMallocDefault));
-            BKD_HIP(hipHostMalloc((void**)&h_len[s], kSegEntries * 4, hipHostMallocDefault));
-            BKD_HIP(hipHostMalloc((void**)&h_seed[s], kSegEntries * 4, hipHostMallocDefault));
-            BKD_HIP(hipHostMalloc((void**)&h_res[s], kSegEntries * 4, hipHostMallocDefault));
-            BKD_HIP(hipMalloc((void**)&d_off[s], kSegEntries * 8));
-            BKD_HIP(hipMalloc((void**)&d_len[s], kSegEntries * 4));
-            BKD_HIP(hipMalloc((void**)&d_seed[s], kSegEntries * 4));
-            BKD_HIP(hipMalloc((void**)&d_res[s], kSegEntries * 4));
-            BKD_HIP(hipStreamCreateWithFlags(&st[s], hipStreamNonBlocking));
-            BKD_HIP(hipEventCreateWithFlags(&done[s], hipEventDisableTiming));
+            if (!h_pin[s]) BKD_HIP(hipHostMalloc((void**)&h_pin[s], kSeg, hipHostMallocDefault));
+            if (!d_buf[s]) BKD_HIP(hipMalloc((void**)&d_buf[s], kSeg));
+            if (!h_off[s]) BKD_HIP(hipHostMalloc((void**)&h_off[s], kSegEntries * 8, hipHostMallocDefault));
+            if (!h_len[s]) BKD_HIP(hipHostMalloc((void**)&h_len[s], kSegEntries * 4, hipHostMallocDefault));
+            if (!h_seed[s]) BKD_HIP(hipHostMalloc((void**)&h_seed[s], kSegEntries * 4, hipHostMallocDefault));
+            if (!h_res[s]) BKD_HIP(hipHostMalloc((void**)&h_res[s], kSegEntries * 4, hipHostMallocDefault));
+            if (!d_off[s]) BKD_HIP(hipMalloc((void**)&d_off[s], kSegEntries * 8));
+            if (!d_len[s]) BKD_HIP(hipMalloc((void**)&d_len[s], kSegEntries * 4));
+            if (!d_seed[s]) BKD_HIP(hipMalloc((void**)&d_seed[s], kSegEntries * 4));
+            if (!d_res[s]) BKD_HIP(hipMalloc((void**)&d_res[s], kSegEntries * 4));
+            if (!st[s]) BKD_HIP(hipStreamCreateWithFlags(&st[s], hipStreamNonBlocking));
+            if (!done[s]) BKD_HIP(hipEventCreateWithFlags(&done[s], hipEventDisableTiming));
         }
         ready = true;
         return BKD_OK;
     }
 };
-HostStage g_stage[kMaxDevices];
+
+// Host-resident batches from concurrent callers each take a staging set of their own (created on
+// demand, at most BKD_HOST_STAGES per device, default 4; a caller beyond that waits for one), so
+// one caller's gather and PCIe copies do not hold up another's (no global lock on the
+// hot path). A set with the framed-entry buffers is ~0.4 GiB of pinned memory.
+struct StagePool {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<std::unique_ptr<HostStage>> all;
+    std::vector<HostStage*> idle;
+};
+StagePool g_stages[kMaxDevices];
+
+size_t max_stages() {
+    static const size_t m = [] {
+        const char* v = getenv("BKD_HOST_STAGES");
+        const int k = v ? atoi(v) : 4;
+        return (size_t)std::max(1, std::min(64, k));
+    }();
+    return m;
+}
+
+// A staging set for the duration of one host-resident call.
+class StageLease {
+  public:
+    explicit StageLease(int dev) : pool_(g_stages[dev]) {
+        std::unique_lock<std::mutex> lk(pool_.mu);
+        pool_.cv.wait(lk, [&] { return !pool_.idle.empty() || pool_.all.size() < max_stages(); });
+        if (!pool_.idle.empty()) {
+            hs_ = pool_.idle.back();
+            pool_.idle.pop_back();
+        } else {
+            pool_.all.emplace_back(new HostStage());
+            hs_ = pool_.all.back().get();
+        }
+    }
+    ~StageLease() {
+        {
+            std::lock_guard<std::mutex> lk(pool_.mu);
+            pool_.idle.push_back(hs_);
+        }
+        pool_.cv.notify_one();
+    }
+    HostStage& operator*() const { return *hs_; }
+
+  private:
+    StagePool& pool_;
+    HostStage* hs_ = nullptr;
+};
 
 // Host threads for the copies into pinned staging (a pageable source, or a list of separate
 // entry buffers such as a ByteBufList): one core copies ~10-20 GB/s, below PCIe Gen5's ~55.
@@ -1152,8 +1201,8 @@ int bkd_crc_batch_host(int algo, const void* h_base, uint64_t base_size, const u
     DeviceState* ds = nullptr;
     int rc = enter(nullptr, scope, &ds);
     if (rc) return rc;
-    HostStage& hs = g_stage[ds - g_dev];
-    std::lock_guard<std::mutex> lk(hs.mu);
+    StageLease lease((int)(ds - g_dev));
+    HostStage& hs = *lease;
     rc = hs.init();
     if (rc) return rc;
     if (!sorted) return host_batch_oneshot(*ds, hs, algo, (const uint8_t*)h_base, base_size, h_offsets, h_lengths, n,
@@ -1302,8 +1351,8 @@ int bkd_digest_verify_batch_host(int algo, int64_t ledger_id, int64_t first_entr
     DeviceState* ds = nullptr;
     int rc = enter(nullptr, scope, &ds);
     if (rc) return rc;
-    HostStage& hs = g_stage[ds - g_dev];
-    std::lock_guard<std::mutex> lk(hs.mu);
+    StageLease lease((int)(ds - g_dev));
+    HostStage& hs = *lease;
     if ((rc = hs.init()) || (rc = hs.init_aux())) return rc;
     const int id_checks = skip_entry_check ? 1 : 0;
     auto seg = [&](int s, uint64_t i0, uint64_t cnt, uint64_t bytes) -> int {
@@ -1346,8 +1395,8 @@ int bkd_digest_package_batch_host(int algo, int64_t ledger_id, const int64_t* h_
     DeviceState* ds = nullptr;
     int rc = enter(nullptr, scope, &ds);
     if (rc) return rc;
-    HostStage& hs = g_stage[ds - g_dev];
-    std::lock_guard<std::mutex> lk(hs.mu);
+    StageLease lease((int)(ds - g_dev));
+    HostStage& hs = *lease;
     if ((rc = hs.init()) || (rc = hs.init_aux())) return rc;
     const uint64_t max_entries = std::min<uint64_t>(HostStage::kSegEntries, HostStage::kAux / frame_stride);
     auto seg = [&](int s, uint64_t i0, uint64_t cnt, uint64_t bytes) -> int {

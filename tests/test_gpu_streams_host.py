@@ -222,6 +222,44 @@ def test_verify_batch_host_matches_oracle(gpu, algo, dtype):
     assert fb == 1700 and (st == 0).all()
 
 
+def test_verify_batch_host_concurrent_callers(gpu):
+    """§8b threading: read completions verify their ByteBufLists from several threads at once; each
+    caller takes a staging set of its own (more callers than sets wait for one); every status and
+    verified prefix equals the oracle's."""
+    algo = ck.CRC32C
+    ledger, first = 17, 500
+    dm = dg.DigestManager.instantiate(ledger, b"", dg.DigestType.CRC32C)
+    rng = np.random.default_rng(91)
+    batches = []
+    for k in range(10):
+        frames = _frames(algo, rng, 200 + 37 * k, ledger, first, 6000)
+        bad = int(rng.integers(0, len(frames)))
+        if k % 2:
+            frames[bad][-1 if len(frames[bad]) > 40 else 33] ^= 0x10
+        want = np.array([oracle.verify_entry(algo, bytes(f), ledger, first + i) for i, f in enumerate(frames)])
+        nz = np.nonzero(want)[0]
+        batches.append((frames, want, int(nz[0]) if nz.size else len(frames)))
+    errors = []
+    barrier = threading.Barrier(len(batches))
+
+    def worker(k):
+        frames, want, fb_want = batches[k]
+        try:
+            barrier.wait()
+            for _ in range(5):
+                st, fb = dm.verify_batch_host(frames, first)
+                assert (st == want).all() and fb == fb_want, k
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(len(batches))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not errors, errors
+
+
 def test_verify_batch_host_many_segments(gpu):
     """> 64 MiB of frames: several double-buffered segments; the first bad entry in a later segment."""
     algo = ck.CRC32C
