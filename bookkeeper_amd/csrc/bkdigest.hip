@@ -1231,14 +1231,19 @@ int bkd_resume_host(int algo, uint32_t current, const void* h_ptr, uint64_t len,
     // entries are indexed with 32-bit lengths: a longer buffer resumes piece by piece
     // (Sse42Crc32C.resume takes a long length, Sse42Crc32C.java:105-107)
     const uint8_t* p = (const uint8_t*)h_ptr;
+    uint32_t r = current;
     for (uint64_t at = 0; at < len;) {
         const uint64_t off = 0;
         const uint32_t l32 = (uint32_t)std::min<uint64_t>(len - at, kResumePiece);
-        const int rc = bkd_crc_batch_host(algo, p + at, l32, &off, &l32, 1, nullptr, current, &current);
+        const int rc = bkd_crc_batch_host(algo, p + at, l32, &off, &l32, 1, nullptr, r, &r);
+        if (rc == BKD_ERR_HIP || rc == BKD_ERR_NOMEM || rc == BKD_ERR_NO_DEVICE)
+            // a device that fails (init, allocation, a copy) degrades to the CPU route, never to an
+            // error: the reference's provider chain never throws (Crc32cIntChecksum.java:28-36)
+            return cpu_resume(algo, current, h_ptr, len, out);
         if (rc) return rc;
         at += l32;
     }
-    *out = current;
+    *out = r;
     return BKD_OK;
 }
 

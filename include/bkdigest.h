@@ -138,7 +138,8 @@ BKD_API int bkd_crc_batch_host(int algo, const void* h_base, uint64_t base_size,
  * ($CJ/checksum/IntHash.java:28-32). len == 0 returns `current` (crc32c_sse42.cpp:211-213).
  *
  * bkd_resume_host: a host buffer. Up to bkd_get_cpu_route_max() bytes, or with no device, the
- *   CPU route (PCLMUL folding / SSE4.2 crc32, host_crc.cpp); above, the GPU through pinned staging.
+ *   CPU route (PCLMUL folding / SSE4.2 crc32, host_crc.cpp); above, the GPU through pinned staging
+ *   (the CPU route again if the device fails: init, allocation or copy errors never surface here).
  * bkd_resume_device: a device buffer, on the caller's `stream` (ordered after the work that
  *   produced the bytes), synchronous. One launch per call: batch callers use bkd_crc_batch.
  * bkd_resume: either; the pointer kind is looked up (hipPointerGetAttributes), and a device
