@@ -261,10 +261,14 @@ def crc_batch_host(algo: int, base, offsets, lengths, seeds=None, seed_all: int 
     offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
     lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
     n = offsets.size
+    if lengths.size != n:
+        raise ValueError("offsets/lengths size mismatch")
     out = np.zeros(n, dtype=np.uint32)
     sp = ctypes.c_void_p(0)
     if seeds is not None:
         seeds = np.ascontiguousarray(seeds, dtype=np.uint32)
+        if seeds.size < n:
+            raise ValueError(f"seeds has {seeds.size} elements, needs {n}")
         sp = ctypes.c_void_p(seeds.ctypes.data)
     check(lib().bkd_crc_batch_host(algo, ctypes.c_void_p(view.ctypes.data if view.size else 0), view.size,
                                    ctypes.c_void_p(offsets.ctypes.data), ctypes.c_void_p(lengths.ctypes.data), n,

@@ -207,3 +207,12 @@ def test_segments_join_model(algo):
                     reg = oracle.gf_mul(algo, pw[b], reg)
             reg ^= raw
         assert (~reg) & 0xFFFFFFFF == oracle.resume(algo, seed, b"".join(segs))
+
+
+def test_host_batch_wrapper_validates_index_sizes():
+    """crc_batch_host refuses index arrays shorter than the batch before the library reads them."""
+    data = bytes(1000)
+    with pytest.raises(ValueError):
+        ck.crc_batch_host(ck.CRC32C, data, [0, 10, 20], [5, 5])
+    with pytest.raises(ValueError):
+        ck.crc_batch_host(ck.CRC32C, data, [0, 10], [5, 5], seeds=[1])
