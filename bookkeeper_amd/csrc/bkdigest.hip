@@ -70,6 +70,21 @@ struct StreamScratch {
     uint32_t* run = nullptr;
     uint32_t* uni = nullptr;  // PlanRun uniform-lengths word (the epoch of the call it holds for)
     uint32_t epoch = 0;
+    // verify gate word (verify_gate_kernel) and the epoch of the latest verify on this stream
+    uint32_t* vflag = nullptr;
+    uint32_t vepoch = 0;
+    hipError_t vflag_word(hipStream_t st, uint32_t** out) {
+        if (!vflag) {
+            hipError_t e = hipMallocAsync((void**)&vflag, sizeof(uint32_t), st);
+            if (e == hipSuccess) e = hipMemsetAsync(vflag, 0, sizeof(uint32_t), st);
+            if (e != hipSuccess) {
+                vflag = nullptr;
+                return e;
+            }
+        }
+        *out = vflag;
+        return hipSuccess;
+    }
     hipError_t run_word(hipStream_t st, uint32_t** out) {
         if (!run) {
             hipError_t e = hipMallocAsync((void**)&run, sizeof(uint32_t), st);
@@ -174,6 +189,9 @@ std::atomic<uint32_t> g_plan_serial{BKD_PLAN_SERIAL};
 #define BKD_SHORT_MEAN_MAX 1024
 #endif
 constexpr uint64_t kShortClassMeanMax = BKD_SHORT_MEAN_MAX;  // bytes of base buffer per entry
+#ifndef BKD_VERIFY_FUSED
+#define BKD_VERIFY_FUSED 1
+#endif
 // Indexed batches whose base buffer is at most this size skip the plan (latency over balance).
 constexpr uint64_t kDirectMaxBytes = 256u << 10;
 
@@ -364,8 +382,12 @@ void launch_plan_chunks(const bkd::PlanRun& run, const uint8_t* base, const bkd:
 // host sync, scratch from the stream's arena.
 int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, const uint64_t* offsets,
                 const uint32_t* lengths, uint64_t n, const uint32_t* seeds, uint32_t seed_all, uint32_t* out,
-                hipStream_t st, bool short_class = true, bool direct_gate = true) {
+                hipStream_t st, bool short_class = true, bool direct_gate = true, const uint32_t* ext_flag = nullptr,
+                uint32_t ext_epoch = 0) {
+    // ext_flag: the plan runs only if *ext_flag == ext_epoch when its kernels start (a gate decided on
+    // the device before this call, verify_framed's); no short class and no uniformity gate then
     if (n == 0) return BKD_OK;
+    if (ext_flag) short_class = direct_gate = false;
     if (n >= 0xFFFFFFF0ull) return fail(BKD_ERR_INVALID_ARG, "indexed batches hold fewer than 2^32 - 16 entries");
     const int G = g_plan_lanes.load();
     bkd::PlanGeo pg;
@@ -416,7 +438,7 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     if (e == hipSuccess && gate) e = sc.uni_word(st, &uni);
     if (e != hipSuccess) return fail(BKD_ERR_NOMEM, std::string("plan scratch: ") + hipGetErrorString(e));
     if (++sc.epoch == 0u) ++sc.epoch;  // 0 is the words' initial value
-    const bkd::PlanRun run{run_word, uni, sc.epoch};
+    const bkd::PlanRun run = ext_flag ? bkd::PlanRun{ext_flag, nullptr, ext_epoch} : bkd::PlanRun{run_word, uni, sc.epoch};
     uint32_t *blk = Carver::at<uint32_t>(sb, o_blk), *blive = Carver::at<uint32_t>(sb, o_live),
              *bok = gate ? Carver::at<uint32_t>(sb, o_bok) : nullptr,
              *blkoff = Carver::at<uint32_t>(sb, o_blkoff), *hdr = Carver::at<uint32_t>(sb, o_hdr),
@@ -462,13 +484,19 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     return BKD_OK;
 }
 
-int indexed_batch(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, const uint64_t* offsets,
-                  const uint32_t* lengths, uint64_t n, const uint32_t* seeds, uint32_t seed_all, uint32_t* out,
-                  hipStream_t st) {
+// The route indexed_batch takes: the direct kernel (one entry per group) or the chunked plan.
+bool indexed_direct(uint64_t size) {
     const int mode = g_plan_mode.load();
     // plan descriptors hold a biased 41-bit window start (PlanDesc): buffers >= 1 TiB take the direct kernel
-    const bool direct = mode == 1 || (mode == 0 && size <= kDirectMaxBytes) || size >= bkd::kPlanMaxSize;
-    if (!direct) return launch_plan(ds, algo, base, size, offsets, lengths, n, seeds, seed_all, out, st);
+    return mode == 1 || (mode == 0 && size <= kDirectMaxBytes) || size >= bkd::kPlanMaxSize;
+}
+
+int indexed_batch(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, const uint64_t* offsets,
+                  const uint32_t* lengths, uint64_t n, const uint32_t* seeds, uint32_t seed_all, uint32_t* out,
+                  hipStream_t st, const uint32_t* ext_flag, uint32_t ext_epoch) {
+    if (!indexed_direct(size))
+        return launch_plan(ds, algo, base, size, offsets, lengths, n, seeds, seed_all, out, st, true, true, ext_flag,
+                           ext_epoch);
     uint32_t* err = nullptr;
     {
         StreamScratch& sc = scratch_for(ds, st);
@@ -708,7 +736,7 @@ void gather_entries(const void* const* src, const uint32_t* len, uint64_t cnt, u
 
 int indexed_batch(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, const uint64_t* offsets,
                   const uint32_t* lengths, uint64_t n, const uint32_t* seeds, uint32_t seed_all, uint32_t* out,
-                  hipStream_t st);
+                  hipStream_t st, const uint32_t* ext_flag = nullptr, uint32_t ext_epoch = 0);
 
 bool is_pinned_host(const void* p) {
     hipPointerAttribute_t attr;
@@ -857,8 +885,25 @@ int package_framed(DeviceState& ds, hipStream_t st, int algo, int64_t ledger_id,
     return BKD_OK;
 }
 
+// Fused verify of near-uniform frames: one kernel per lane count (crc_verify_fused_kernel).
+template <int G>
+void launch_verify_fused(DeviceState& ds, hipStream_t st, int algo, const uint8_t* framed, uint64_t size,
+                         const uint64_t* offsets, const uint32_t* lengths, uint64_t n, uint32_t mac, int64_t ledger_id,
+                         int64_t first_entry_id, int id_checks, int32_t* status, uint64_t* first_bad,
+                         const uint32_t* vflag, uint32_t vepoch) {
+    const uint64_t per_block = bkd::kBlock / G;
+    const unsigned blocks = (unsigned)std::min<uint64_t>((n + per_block - 1) / per_block, (uint64_t)ds.cus);
+    hipLaunchKernelGGL((bkd::crc_verify_fused_kernel<G, kPF, kNT>), dim3(blocks), dim3(bkd::kBlock), 0, st, framed, size,
+                       offsets, lengths, n, mac, ledger_id, first_entry_id, id_checks, ds.tables[algo][lane_index(G)],
+                       status, (unsigned long long*)first_bad, vflag, vepoch);
+}
+
 // Verify (bkd_digest_verify_batch and bkd_entrylog_verify): header CRCs -> payload CRCs seeded
-// with them through the indexed path (chunked plan for large ragged batches) -> compare.
+// with them through the indexed path (chunked plan for large ragged batches) -> compare. Batches
+// that take the plan route first run a gate over the frame lengths: when every frame is within
+// PlanRun::in_band of the first, the fused kernel verifies each frame whole (header, payload and
+// compare in one pass over it) and the header / plan / finish kernels return at once; otherwise
+// the fused kernel returns and they run. Both give the same statuses; the device decides, no sync.
 int verify_framed(DeviceState& ds, hipStream_t st, int algo, int64_t ledger_id, int64_t first_entry_id,
                   int id_checks, const void* d_framed, uint64_t framed_size, const uint64_t* d_offsets,
                   const uint32_t* d_lengths, uint64_t n, int32_t* d_status, uint64_t* d_first_bad) {
@@ -882,18 +927,48 @@ int verify_framed(DeviceState& ds, hipStream_t st, int algo, int64_t ledger_id, 
     uint64_t* poff = Carver::at<uint64_t>(sb, o_poff);
     uint32_t* expect = Carver::at<uint32_t>(sb, o_exp);
     uint32_t* pre = Carver::at<uint32_t>(sb, o_pre);
+    // the fused route where the payloads would take the plan (large batches; the direct kernel's small
+    // ones keep the three-kernel sequence)
+    const int fused_lanes = auto_lanes(framed_size / n, n, ds.cus);
+    const bool fused = BKD_VERIFY_FUSED && !indexed_direct(framed_size);
+    uint32_t* vflag = nullptr;
+    uint32_t vepoch = 0;
+    if (fused) {
+        e = sc.vflag_word(st, &vflag);
+        if (e != hipSuccess) return fail(BKD_ERR_NOMEM, std::string("verify gate: ") + hipGetErrorString(e));
+        if (++sc.vepoch == 0u) ++sc.vepoch;  // 0 is the word's initial value
+        vepoch = sc.vepoch;
+        const unsigned gblocks = (unsigned)std::min<uint64_t>((n + 1023) / 1024, (uint64_t)ds.cus);
+        hipLaunchKernelGGL(bkd::verify_gate_kernel, dim3(gblocks), dim3(1024), 0, st, d_lengths, n, d_first_bad, vflag,
+                           vepoch);
+        const uint8_t* fb = (const uint8_t*)d_framed;
+        switch (fused_lanes) {
+            case 4: launch_verify_fused<4>(ds, st, algo, fb, framed_size, d_offsets, d_lengths, n, mac, ledger_id,
+                                           first_entry_id, id_checks, d_status, d_first_bad, vflag, vepoch); break;
+            case 8: launch_verify_fused<8>(ds, st, algo, fb, framed_size, d_offsets, d_lengths, n, mac, ledger_id,
+                                           first_entry_id, id_checks, d_status, d_first_bad, vflag, vepoch); break;
+            case 16: launch_verify_fused<16>(ds, st, algo, fb, framed_size, d_offsets, d_lengths, n, mac, ledger_id,
+                                             first_entry_id, id_checks, d_status, d_first_bad, vflag, vepoch); break;
+            case 32: launch_verify_fused<32>(ds, st, algo, fb, framed_size, d_offsets, d_lengths, n, mac, ledger_id,
+                                             first_entry_id, id_checks, d_status, d_first_bad, vflag, vepoch); break;
+            default: launch_verify_fused<64>(ds, st, algo, fb, framed_size, d_offsets, d_lengths, n, mac, ledger_id,
+                                             first_entry_id, id_checks, d_status, d_first_bad, vflag, vepoch); break;
+        }
+        e = hipGetLastError();
+        if (e != hipSuccess) return fail(BKD_ERR_HIP, hipGetErrorString(e));
+    }
     const unsigned hblocks = (unsigned)std::min<uint64_t>((n + 1023) / 1024, 2u * (uint64_t)ds.cus);
     hipLaunchKernelGGL(bkd::verify_header_kernel, dim3(hblocks), dim3(1024), 0, st, x32tab, (const uint8_t*)d_framed,
                        framed_size, d_offsets, d_lengths, n, mac, ledger_id, first_entry_id, id_checks, seeds, poff,
-                       plen, expect, pre, d_first_bad);
+                       plen, expect, pre, d_first_bad, vflag, vepoch);
     e = hipGetLastError();
     if (e != hipSuccess) return fail(BKD_ERR_HIP, hipGetErrorString(e));
     // payload CRCs land in d_status, then verify_finish turns them into status codes
     int rc = indexed_batch(ds, algo, (const uint8_t*)d_framed, framed_size, poff, plen, n, seeds, 0,
-                           reinterpret_cast<uint32_t*>(d_status), st);
+                           reinterpret_cast<uint32_t*>(d_status), st, vflag, vepoch);
     if (rc) return rc;
     hipLaunchKernelGGL(bkd::verify_finish_kernel, dim3(blocks), dim3(256), 0, st, expect, pre, n, d_status,
-                       (unsigned long long*)d_first_bad);
+                       (unsigned long long*)d_first_bad, vflag, vepoch);
     e = hipGetLastError();
     if (e != hipSuccess) return fail(BKD_ERR_HIP, hipGetErrorString(e));
     return BKD_OK;
@@ -1177,7 +1252,7 @@ int bkd_stream_release(void* stream) {
         // stream-ordered allocations go back the way they came
         for (int k = 0; k < 3; ++k)
             if (sc->buf[k]) BKD_HIP(hipFreeAsync(sc->buf[k], st));
-        for (uint32_t* w : {sc->err, sc->run, sc->uni})
+        for (uint32_t* w : {sc->err, sc->run, sc->uni, sc->vflag})
             if (w) BKD_HIP(hipFreeAsync(w, st));
         BKD_HIP(hipStreamSynchronize(st));
         if (sc->h_err) BKD_HIP(hipHostFree(sc->h_err));

@@ -345,6 +345,62 @@ def test_digest_batch_package_and_verify(gpu, dtype, algo):
     assert status[1234] != 0 and int(first_bad.item()) == 1234
 
 
+@pytest.mark.parametrize("dtype,algo", [(dg.DigestType.CRC32C, ck.CRC32C), (dg.DigestType.CRC32, ck.CRC32)])
+@pytest.mark.parametrize("skip", [False, True])
+def test_verify_batch_near_uniform_frames(gpu, dtype, algo, skip):
+    """Frames whose lengths all lie in the near-uniform band take the fused verify (gate -> one kernel
+    per frame: header CRC, payload, compare); one frame out of band sends the same batch through the
+    header / plan / finish sequence. Both give oracle.verify_entry's status for every frame and the
+    verified prefix, with every failure kind: payload and digest bytes, CRC32's high digest word,
+    ledger id, entry id, a frame past the buffer's end; unaligned frame offsets."""
+    import torch
+    rng = np.random.default_rng(40 + algo + 2 * skip)
+    n, ledger, first = 6000, 31, 9000
+    dm = dg.DigestManager.instantiate(ledger, b"", dtype, False)
+    mac = dm.macCodeLength
+    plen = rng.integers(3950, 4150, n)  # within 1/16 of each other: the fused route
+    payload = oracle.fill_splitmix64(int(plen.sum()), 23)
+    poffs = np.concatenate([[0], np.cumsum(plen[:-1])])
+    frames = []
+    for i in range(n):
+        p = payload[poffs[i]:poffs[i] + plen[i]]
+        d, hdr = oracle.digest_entry(algo, ledger, first + i, first + i - 1, int(plen[i]), p)
+        frames.append(bytearray(hdr + oracle.digest_bytes(algo, d) + p.tobytes()))
+    frames[4000][40 + mac] ^= 0x01  # payload
+    frames[4500][32 + mac - 1] ^= 0x80  # digest
+    frames[5000][7] ^= 0x02  # ledger id
+    frames[5500][15] ^= 0x04  # entry id (passes when skip)
+    if algo == ck.CRC32:
+        frames[5900][33] ^= 0x10  # the zero high word of the 8-byte digest
+    gaps = rng.integers(0, 13, n)  # unaligned frame offsets
+    flens = np.array([len(f) for f in frames], dtype=np.int64)
+    foffs = np.concatenate([[0], np.cumsum(flens[:-1] + gaps[:-1])]) + 5
+    blob = np.zeros(int(foffs[-1] + flens[-1]) + 64, dtype=np.uint8)
+    for i in range(n):
+        blob[foffs[i]:foffs[i] + flens[i]] = np.frombuffer(bytes(frames[i]), dtype=np.uint8)
+    want = np.array([oracle.verify_entry(algo, bytes(frames[i]), ledger, first + i, skip) for i in range(n)])
+    foffs_oob = foffs.copy()
+    foffs_oob[5800] = blob.size - 100  # the frame would run past the buffer: VERIFY_TOO_SHORT
+    want_oob = want.copy()
+    want_oob[5800] = 1
+    d_blob = _dev_bytes(torch, blob, gpu)
+    d_len = torch.from_numpy(flens.astype(np.int32)).to(gpu)
+    cases = [(foffs_oob, d_len, want_oob)]
+    flens_mixed = flens.copy()  # one frame far out of band: the header / plan / finish route
+    flens_mixed[10] = 100
+    want_mixed = want_oob.copy()
+    want_mixed[10] = oracle.verify_entry(algo, bytes(frames[10][:100]), ledger, first + 10, skip)
+    cases.append((foffs_oob, torch.from_numpy(flens_mixed.astype(np.int32)).to(gpu), want_mixed))
+    for offs, d_l, w in cases:
+        status, first_bad = dm.verify_batch(d_blob, torch.from_numpy(offs).to(gpu), d_l, first_entry_id=first,
+                                            skip_entry_check=skip)
+        status = status.cpu().numpy()
+        bad = np.nonzero(status != w)[0]
+        assert bad.size == 0, (bad[:5], status[bad[:5]], w[bad[:5]])
+        nz = np.nonzero(w)[0]
+        assert int(first_bad.item()) == (int(nz[0]) if nz.size else n)
+
+
 def test_plan_overflow_falls_back_to_direct(gpu):
     """Heavily overlapping entries exceed the plan's capacity (n + size/CH + 16 chunks); the
     overflowing entries are computed one entry per group in the chunk kernel's tail, bit-exact."""
