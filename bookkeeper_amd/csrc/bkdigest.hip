@@ -510,12 +510,14 @@ int indexed_batch(DeviceState& ds, int algo, const uint8_t* base, uint64_t size,
 
 bool valid_algo(int algo) { return algo == BKD_CRC32C || algo == BKD_CRC32; }
 
-bool is_device_pointer(const void* p) {
+// Whether p is device memory; *dev (if given) = the device it lives on.
+bool is_device_pointer(const void* p, int* dev = nullptr) {
     hipPointerAttribute_t attr;
     if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
         (void)hipGetLastError();
         return false;
     }
+    if (dev) *dev = attr.device;
     return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
 }
 
@@ -1351,8 +1353,18 @@ int bkd_resume(int algo, uint32_t current, const void* ptr, uint64_t len, uint32
     if (!ptr) return fail(BKD_ERR_INVALID_ARG, "null buffer");
     // a device buffer runs on the null stream, which orders the call after the work queued on
     // the blocking streams (PyTorch's default stream among them) that may still be writing it
-    if (visible_devices() > 0 && is_device_pointer(ptr))
+    int pdev = -1;
+    if (visible_devices() > 0 && is_device_pointer(ptr, &pdev)) {
+        // on the null stream of the device that holds the buffer (not whichever is current)
+        int cur = 0;
+        BKD_HIP(hipGetDevice(&cur));
+        DeviceScope scope;
+        if (pdev >= 0 && pdev != cur) {
+            BKD_HIP(hipSetDevice(pdev));
+            scope.prev = cur;
+        }
         return bkd_resume_device(algo, current, ptr, len, nullptr, out);
+    }
     return bkd_resume_host(algo, current, ptr, len, out);
 }
 

@@ -143,7 +143,8 @@ BKD_API int bkd_crc_batch_host(int algo, const void* h_base, uint64_t base_size,
  * bkd_resume_device: a device buffer, on the caller's `stream` (ordered after the work that
  *   produced the bytes), synchronous. One launch per call: batch callers use bkd_crc_batch.
  * bkd_resume: either; the pointer kind is looked up (hipPointerGetAttributes), and a device
- *   buffer runs on the null stream, which orders it after work on the blocking streams.
+ *   buffer runs on the null stream of the device that holds it, which orders it after work on
+ *   that device's blocking streams.
  * bkd_cpu_resume: always the CPU route (no device needed). */
 BKD_API int bkd_resume(int algo, uint32_t current, const void* ptr, uint64_t len, uint32_t* out);
 BKD_API int bkd_resume_host(int algo, uint32_t current, const void* h_ptr, uint64_t len, uint32_t* out);
