@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define BKD_ABI_VERSION 2
+#define BKD_ABI_VERSION 3
 
 /* only the entry points below are exported (the library is built with -fvisibility=hidden) */
 #ifndef BKD_API

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     assert set(declared) <= exported
     # nothing but the declared entry points leaks as a C symbol (C++ kernel stubs are mangled)
     assert {x for x in exported if not x.startswith("_Z") and not x.startswith("__hip")} == set(declared)
-    assert L.bkd_abi_version() == 2
+    assert L.bkd_abi_version() == 3  # 3: bkd_stream_release
 
 
 def test_library_contains_gfx950_code():
