@@ -1037,7 +1037,6 @@ int cpu_resume(int algo, uint32_t current, const void* p, uint64_t len, uint32_t
 // Device scratch of one synchronous per-call resume, pooled per device (no per-thread state
 // that outlives its thread, no allocation on the hot path after the first calls).
 struct CallScratch {
-    uint32_t* d_out = nullptr;
     uint64_t* d_off = nullptr;
     uint32_t* d_len = nullptr;
     uint32_t* h_out = nullptr;  // pinned: [0] result, [1] length for the plan path
@@ -1059,7 +1058,6 @@ int call_acquire(int dev, hipStream_t st, CallScratch** out) {
         }
     }
     std::unique_ptr<CallScratch> c(new CallScratch());
-    BKD_HIP(hipMalloc((void**)&c->d_out, 4));
     BKD_HIP(hipMalloc((void**)&c->d_off, 8));
     BKD_HIP(hipMalloc((void**)&c->d_len, 4));
     BKD_HIP(hipHostMalloc((void**)&c->h_out, 8, hipHostMallocDefault));
@@ -1082,21 +1080,23 @@ int resume_device(int algo, uint32_t current, const void* ptr, uint64_t len, hip
     CallScratch* c = nullptr;
     if ((rc = call_acquire(dev, st, &c))) return rc;
     const uint32_t l32 = (uint32_t)len;
+    // the kernel stores the digest straight into the pinned host word (no D2H copy on the call's
+    // critical path; visible to the host once the stream has synchronised)
+    uint32_t* res = c->h_out;
     if (len < (1u << 20)) {  // one group: the entry as a uniform batch of one
-        bkd::UniformSrc src{1, len, l32, nullptr, current, c->d_out};
+        bkd::UniformSrc src{1, len, l32, nullptr, current, res};
         rc = dispatch_lanes(*ds, auto_lanes(len, 1, ds->cus), algo, (const uint8_t*)ptr, src, 1, st);
     } else {  // large: the chunked plan spreads it over the chip
         c->h_out[1] = l32;
         const hipError_t e = hipMemcpyAsync(c->d_len, c->h_out + 1, 4, hipMemcpyHostToDevice, st);
         rc = e == hipSuccess ? launch_plan(*ds, algo, (const uint8_t*)ptr, len, c->d_off, c->d_len, 1, nullptr,
-                                           current, c->d_out, st, false, false)
+                                           current, res, st, false, false)
                              : fail(BKD_ERR_HIP, hipGetErrorString(e));
     }
     if (!rc) {
-        hipError_t e = hipMemcpyAsync(c->h_out, c->d_out, 4, hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        const hipError_t e = hipStreamSynchronize(st);
         if (e != hipSuccess) rc = fail(BKD_ERR_HIP, std::string("resume: ") + hipGetErrorString(e));
-        else *out = c->h_out[0];
+        else *out = __atomic_load_n(c->h_out, __ATOMIC_ACQUIRE);
     }
     call_release(dev, c);
     return rc;
