@@ -705,10 +705,20 @@ class CopyPool {
     bool stop_ = false;
 };
 
-// memcpy of one range on the copy pool (parts of >= 4 MiB).
+// Bytes per copy-pool part (BKD_COPY_PART_KIB overrides the default).
+size_t copy_part_bytes() {
+    static const size_t b = [] {
+        const char* v = getenv("BKD_COPY_PART_KIB");
+        const long k = v ? atol(v) : 4096;
+        return (size_t)std::max(64L, std::min(1L << 20, k)) << 10;
+    }();
+    return b;
+}
+
+// memcpy of one range on the copy pool (parts of >= copy_part_bytes()).
 void parallel_copy(uint8_t* dst, const uint8_t* src, size_t n) {
     CopyPool& pool = CopyPool::get();
-    const int parts = (int)std::min<size_t>((size_t)pool.threads(), std::max<size_t>(1, n >> 22));
+    const int parts = (int)std::min<size_t>((size_t)pool.threads(), std::max<size_t>(1, n / copy_part_bytes()));
     const size_t per = (n + parts - 1) / parts;
     pool.run(parts, [&](int p) {
         const size_t a = std::min(n, per * (size_t)p), b = std::min(n, a + per);
@@ -725,7 +735,7 @@ void gather_entries(const void* const* src, const uint32_t* len, uint64_t cnt, u
         at += len[i];
     }
     CopyPool& pool = CopyPool::get();
-    const int parts = (int)std::min<uint64_t>((uint64_t)pool.threads(), std::max<uint64_t>(1, at >> 22));
+    const int parts = (int)std::min<uint64_t>((uint64_t)pool.threads(), std::max<uint64_t>(1, at / copy_part_bytes()));
     const uint64_t per = (at + parts - 1) / parts;
     pool.run(parts, [&](int p) {
         // entries whose first byte lies in [p*per, (p+1)*per)
