@@ -215,10 +215,13 @@ def entrylog_scan(log, start: int = 1024):
     """DefaultEntryLogger.scanEntryLog restated: (offsets u64, lengths u32, ledger ids i64, end)."""
     a = _as_u8(log)
     cap = max(1, a.size // 16)
-    offs = np.zeros(cap, dtype=np.uint64)
-    lens = np.zeros(cap, dtype=np.uint32)
-    lids = np.zeros(cap, dtype=np.int64)
-    end = np.zeros(1, dtype=np.uint64)
-    n = int(lib().oracle_entrylog_scan(_ptr(a, _u8p), a.size, start, _ptr(offs, _u64p), _ptr(lens, _u32p),
-                                       lids.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), cap, _ptr(end, _u64p)))
-    return offs[:n], lens[:n], lids[:n], int(end[0])
+    while True:  # the walk counts past `cap`: a log of tinier records is walked again with room for all
+        offs = np.zeros(cap, dtype=np.uint64)
+        lens = np.zeros(cap, dtype=np.uint32)
+        lids = np.zeros(cap, dtype=np.int64)
+        end = np.zeros(1, dtype=np.uint64)
+        n = int(lib().oracle_entrylog_scan(_ptr(a, _u8p), a.size, start, _ptr(offs, _u64p), _ptr(lens, _u32p),
+                                           lids.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), cap, _ptr(end, _u64p)))
+        if n <= cap:
+            return offs[:n], lens[:n], lids[:n], int(end[0])
+        cap = n

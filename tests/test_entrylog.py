@@ -70,3 +70,20 @@ def test_scrub_skips_untyped_ledgers(gpu):
     scan, status = scrub.verify(np.frombuffer(log, dtype=np.uint8))
     for k, (lid, *_rest) in enumerate(expect):
         assert status[k] == (0 if lid == 3 else -1)
+
+
+def test_scan_many_tiny_records():
+    """a log of records far smaller than 16 bytes (a corrupt or synthetic log) is walked
+    whole — the index grows past the first size//256 guess instead of failing with BKD_ERR_BOUNDS."""
+    rng = np.random.default_rng(12)
+    parts = [bytes(1024)]
+    n = 20000
+    for _ in range(n):
+        size = int(rng.integers(8, 16))
+        parts.append(size.to_bytes(4, "big") + (3).to_bytes(8, "big") + bytes(size - 8))
+    log = b"".join(parts)
+    got = el.scan_entry_log(log)
+    offs, lens, lids, end = oracle.entrylog_scan(log)
+    assert len(got) == len(offs) == n
+    assert (got.offsets == offs).all() and (got.lengths == lens).all() and (got.ledger_ids == lids).all()
+    assert got.end == end
