@@ -955,6 +955,7 @@ int verify_framed(DeviceState& ds, hipStream_t st, int algo, int64_t ledger_id, 
                            vepoch);
         const uint8_t* fb = (const uint8_t*)d_framed;
         switch (fused_lanes) {
+            case 1:  // (a forced one-lane geometry: the fused kernel's narrowest group)
             case 4: launch_verify_fused<4>(ds, st, algo, fb, framed_size, d_offsets, d_lengths, n, mac, ledger_id,
                                            first_entry_id, id_checks, d_status, d_first_bad, vflag, vepoch); break;
             case 8: launch_verify_fused<8>(ds, st, algo, fb, framed_size, d_offsets, d_lengths, n, mac, ledger_id,
