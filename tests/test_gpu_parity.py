@@ -345,6 +345,33 @@ def test_digest_batch_package_and_verify(gpu, dtype, algo):
     assert status[1234] != 0 and int(first_bad.item()) == 1234
 
 
+@pytest.mark.parametrize("dtype,algo,stride", [(dg.DigestType.CRC32C, ck.CRC32C, 37), (dg.DigestType.CRC32, ck.CRC32, 43),
+                                               (dg.DigestType.CRC32C, ck.CRC32C, 128)])
+def test_package_batch_frame_strides(gpu, dtype, algo, stride):
+    """Frames at odd strides (byte stores) and a wide stride, every length class incl. payloads under
+    16 bytes: header and digest bytes equal the oracle's."""
+    import torch
+    rng = np.random.default_rng(stride)
+    n = 5000
+    lens = rng.integers(0, 9000, n)
+    lens[:6] = [0, 1, 15, 16, 17, 4096]
+    offs = np.concatenate([[0], np.cumsum(lens[:-1])]).astype(np.int64)
+    payload = oracle.fill_splitmix64(int(lens.sum()) + 64, 29)
+    dm = dg.DigestManager.instantiate(5, b"", dtype, False)
+    ids = np.arange(n, dtype=np.int64) + 40
+    frames, digests = dm.package_batch(torch.from_numpy(ids).to(gpu), torch.from_numpy(ids - 1).to(gpu),
+                                       torch.from_numpy(lens.astype(np.int64)).to(gpu), _dev_bytes(torch, payload, gpu),
+                                       torch.from_numpy(offs).to(gpu), torch.from_numpy(lens.astype(np.int32)).to(gpu),
+                                       frame_stride=stride, sync_check=True)
+    frames = frames.cpu().numpy()
+    digests = digests.cpu().numpy().view(np.uint32)
+    hl = 32 + dm.macCodeLength
+    for i in range(n):
+        d, hdr = oracle.digest_entry(algo, 5, int(ids[i]), int(ids[i]) - 1, int(lens[i]), payload[offs[i]:offs[i] + lens[i]])
+        assert digests[i] == d, i
+        assert frames[i, :hl].tobytes() == hdr + oracle.digest_bytes(algo, d), i
+
+
 @pytest.mark.parametrize("dtype,algo", [(dg.DigestType.CRC32C, ck.CRC32C), (dg.DigestType.CRC32, ck.CRC32)])
 @pytest.mark.parametrize("skip", [False, True])
 def test_verify_batch_near_uniform_frames(gpu, dtype, algo, skip):
