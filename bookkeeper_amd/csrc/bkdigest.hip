@@ -941,8 +941,10 @@ int verify_framed(DeviceState& ds, hipStream_t st, int algo, int64_t ledger_id, 
     uint32_t* pre = Carver::at<uint32_t>(sb, o_pre);
     // the fused route where the payloads would take the plan (large batches; the direct kernel's small
     // ones keep the three-kernel sequence)
+    // — and, as the plan's own near-uniform gate, only where one frame per group uses the plan's lane
+    // count: a few huge frames need the plan's chunks to fill the chip
     const int fused_lanes = auto_lanes(framed_size / n, n, ds.cus);
-    const bool fused = BKD_VERIFY_FUSED && !indexed_direct(framed_size);
+    const bool fused = BKD_VERIFY_FUSED && !indexed_direct(framed_size) && fused_lanes == g_plan_lanes.load();
     uint32_t* vflag = nullptr;
     uint32_t vepoch = 0;
     if (fused) {

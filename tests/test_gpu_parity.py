@@ -382,7 +382,7 @@ def test_verify_batch_near_uniform_frames(gpu, dtype, algo, skip):
     ledger id, entry id, a frame past the buffer's end; unaligned frame offsets."""
     import torch
     rng = np.random.default_rng(40 + algo + 2 * skip)
-    n, ledger, first = 6000, 31, 9000
+    n, ledger, first = 33000, 31, 9000  # n x 8 lanes >= the chip's lane slots: the fused route
     dm = dg.DigestManager.instantiate(ledger, b"", dtype, False)
     mac = dm.macCodeLength
     plen = rng.integers(3950, 4150, n)  # within 1/16 of each other: the fused route
