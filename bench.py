@@ -407,13 +407,21 @@ def digest_bench(args, ck, torch, rank, dev, stream, algo) -> None:
         raise SystemExit("VERIFY FAILURE: freshly packaged entries did not verify")
 
 
+def default_config(gpus: int, world: int) -> str:
+    """The workload without --config: BASELINE configs[1] (1M x 4 KiB) on one GPU; on several,
+    configs[3] — 64M x 4 KiB split evenly over 8 GPUs = 8M entries (32 GiB) per GPU, weak scaling
+    (SURVEY §8d row 4), so the driver's N = 2/4/8 runs measure config 4's per-GPU shard."""
+    return "shard8m" if max(gpus, world) > 1 else "uniform4k"
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--config", default="uniform4k",
-                    choices=["uniform4k", "shard8m", "zipf", "indexed4k", "host4k", "verify4k", "verify4k_host"])
+    ap.add_argument("--config", default=None,
+                    choices=["uniform4k", "shard8m", "zipf", "indexed4k", "host4k", "verify4k", "verify4k_host"],
+                    help="default: uniform4k (config 2) at N = 1, shard8m (config 4's 8M x 4 KiB per GPU) at N > 1")
     ap.add_argument("--algo", default="crc32c", choices=["crc32c", "crc32"])
     ap.add_argument("--entries", type=int, default=0, help="entries per GPU (default by config)")
     ap.add_argument("--lanes", type=int, default=0, help="force lanes per entry group (0 = auto)")
@@ -428,6 +436,8 @@ def main() -> None:
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         raise SystemExit(self_launch(args.gpus, sys.argv[1:]))
+    if args.config is None:
+        args.config = default_config(args.gpus, int(os.environ.get("WORLD_SIZE", "1")))
 
     import torch
     import torch.distributed as dist
@@ -447,9 +457,20 @@ def main() -> None:
     torch.cuda.set_device(dev)
     if world > 1:
         if args.dist_backend == "nccl":
+            # RCCL; device_id binds this rank's communicator to its GPU up front (no lazy init on the
+            # first collective). Only timing crosses ranks: barriers, one MAX, one all_gather.
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+    try:
+        run_rank(args, ck, torch, dist, world, rank, dev)
+    finally:  # every exit path, a parity failure's SystemExit included
+        if world > 1 and dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def run_rank(args, ck, torch, dist, world: int, rank: int, dev) -> None:
+    """One rank's benchmark (world == 1: the whole job)."""
     algo = ck.CRC32C if args.algo == "crc32c" else ck.CRC32
     ck.set_group_lanes(args.lanes)
     ck.set_plan_mode(args.plan_mode)
@@ -474,8 +495,14 @@ def main() -> None:
         def step():
             ck.crc_batch_uniform(algo, base, entry_len, n, out=out, stream=stream)
         kernel_name = "crc_groups_kernel"
-        workload = {"workload": f"{n} x {entry_len} B ledger entries per GPU, device-resident, {args.algo}, seed 0",
-                    "entries_per_gpu": n, "entry_bytes": entry_len}
+        if args.config == "shard8m":
+            workload = {"workload": f"config 4: 64M x 4 KiB over 8 GPUs, 8M per GPU (this run: {world} GPU"
+                                    f"{'s' if world > 1 else ''} x {n} entries = {n * world} x 4 KiB, weak scaling), "
+                                    f"device-resident, {args.algo}, seed 0",
+                        "entries_per_gpu": n, "entry_bytes": entry_len}
+        else:
+            workload = {"workload": f"{n} x {entry_len} B ledger entries per GPU, device-resident, {args.algo}, seed 0",
+                        "entries_per_gpu": n, "entry_bytes": entry_len}
     else:
         n = args.entries or (1 << 20)
         if args.config == "indexed4k":  # diagnostic: the uniform layout through the indexed (plan) path
@@ -599,8 +626,6 @@ def main() -> None:
             raise SystemExit("PARITY FAILURE: GPU digests differ from the CPU baseline's")
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
 
 
 def _pmc_traffic(config: str):

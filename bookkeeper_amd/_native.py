@@ -1,10 +1,10 @@
 """ctypes binding of libbkdigest.so (include/bkdigest.h).
 
 There is deliberately no Python fallback: if the library is missing, every call raises
-NativeUnavailable. Inside the library, batch calls always run on the GPU (BKD_ERR_NO_DEVICE
-without one); only the per-call host-buffer resume has the library's own native CPU route
-(host_crc.cpp), the role the reference's JNI SSE4.2 provider plays in its selection chain
-(Crc32cIntChecksum.java:28-36).
+NativeUnavailable. Inside the library, device-resident batch calls always run on the GPU
+(BKD_ERR_NO_DEVICE without one); host-resident batches and the per-call host-buffer resume have the
+library's own native CPU route (host_crc.cpp, host_batch.cpp), the role the reference's JNI SSE4.2
+provider plays in its selection chain (Crc32cIntChecksum.java:28-36).
 """
 from __future__ import annotations
 
@@ -86,6 +86,11 @@ PROTOTYPES = {
     "bkd_set_plan_small": (_int, [_u32]),
     "bkd_set_plan_serial": (_int, [_u32]),
     "bkd_get_group_lanes": (_int, [_int, _u64]),
+    "bkd_set_host_batch_route": (_int, [_int]),
+    "bkd_get_host_batch_route": (_int, []),
+    "bkd_set_host_threads": (_int, [_int]),
+    "bkd_get_host_threads": (_int, []),
+    "bkd_host_release": (_int, []),
 }
 
 _lib = None

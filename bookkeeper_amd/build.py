@@ -14,9 +14,10 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libbkdigest.so")
 SOURCES = [os.path.join(CSRC, "bkdigest.hip")]
-HOST_SOURCES = [os.path.join(CSRC, "host_crc.cpp")]  # CPU route (plain C++, built with the host compiler)
+# CPU route and host worker pool (plain C++, built with the host compiler)
+HOST_SOURCES = [os.path.join(CSRC, "host_crc.cpp"), os.path.join(CSRC, "host_batch.cpp")]
 DEPS = SOURCES + HOST_SOURCES + [os.path.join(CSRC, f) for f in (
-    "crc_kernels.hpp", "crc_tables.hpp", "plan_kernels.hpp", "host_crc.hpp")] + [os.path.join(ROOT, "include", "bkdigest.h")]
+    "crc_kernels.hpp", "crc_tables.hpp", "plan_kernels.hpp", "host_crc.hpp", "host_batch.hpp")] + [os.path.join(ROOT, "include", "bkdigest.h")]
 ARCH = os.environ.get("BKD_OFFLOAD_ARCH", "gfx950")
 
 
@@ -48,7 +49,8 @@ def build_native(force: bool = False, extra_flags: list[str] | None = None, out:
     objs = []
     for src in HOST_SOURCES:
         obj = os.path.join(CSRC, os.path.splitext(os.path.basename(src))[0] + f"_{os.getpid()}.o")
-        subprocess.run([cxx(), "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-c", src, "-o", obj], check=True)
+        subprocess.run([cxx(), "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-pthread", "-c", src, "-o", obj],
+                       check=True)
         objs.append(obj)
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden",
            "-I", os.path.join(ROOT, "include"), "-o", out + ".tmp"] + objs + SOURCES + ["-lpthread"] + list(

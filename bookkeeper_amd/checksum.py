@@ -256,7 +256,8 @@ def crc_batch_segments(algo: int, base, seg_offsets, seg_lengths, seg_first, see
 
 
 def crc_batch_host(algo: int, base, offsets, lengths, seeds=None, seed_all: int = 0) -> np.ndarray:
-    """Host-memory batch (H2D -> kernel -> D2H inside the library); returns uint32 CRCs."""
+    """Host-memory batch; returns uint32 CRCs. Route (set_host_batch_route): the GPU (H2D -> kernel
+    -> D2H inside the library) or the library's threaded CPU route."""
     view = _host_view(base)
     offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
     lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
@@ -304,6 +305,47 @@ def cpu_resume(algo: int, current: int, buffer) -> int:
     check(lib().bkd_cpu_resume(algo, current & 0xFFFFFFFF, ctypes.c_void_p(view.ctypes.data if view.size else 0),
                                view.size, ctypes.byref(out)))
     return to_java_int(out.value)
+
+
+HOST_ROUTE_AUTO, HOST_ROUTE_CPU, HOST_ROUTE_GPU = 0, 1, 2
+_host_route = HOST_ROUTE_AUTO  # the route last set through this module
+
+
+def set_host_batch_route(route: int) -> None:
+    """Route of host-resident batches: 0 auto (measured crossover), 1 CPU threads, 2 GPU."""
+    global _host_route
+    check(lib().bkd_set_host_batch_route(route))
+    _host_route = route
+
+
+def get_host_batch_route() -> int:
+    """The route the next host-resident batch takes: 1 CPU, 2 GPU."""
+    return int(lib().bkd_get_host_batch_route())
+
+
+@contextlib.contextmanager
+def host_batch_route(route: int):
+    """Temporarily force the host-resident batch route (tests, benchmarks); restores the previous one."""
+    prev = _host_route
+    set_host_batch_route(route)
+    try:
+        yield
+    finally:
+        set_host_batch_route(prev)
+
+
+def set_host_threads(threads: int) -> None:
+    """Host threads the CPU route and staging copies may use (0 = the whole pool)."""
+    check(lib().bkd_set_host_threads(threads))
+
+
+def get_host_threads() -> int:
+    return int(lib().bkd_get_host_threads())
+
+
+def host_release() -> None:
+    """Frees the idle pinned staging sets of the host batches' GPU route (bkd_host_release)."""
+    check(lib().bkd_host_release())
 
 
 def set_cpu_route_max(nbytes: int) -> None:

@@ -17,6 +17,7 @@
 #include <memory>
 #include <mutex>
 #include <new>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -25,6 +26,7 @@
 #include "crc_kernels.hpp"
 #include "plan_kernels.hpp"
 #include "crc_tables.hpp"
+#include "host_batch.hpp"
 #include "host_crc.hpp"
 
 namespace {
@@ -153,16 +155,20 @@ struct Carver {
     }
 };
 
+// Per device: tables uploaded once (under g_mu, published by `ready`), then read-only; the two maps
+// below grow on first use of an (algo, chunk size) or a stream and are read under a shared lock, so
+// concurrent callers on their own streams never serialise on a process-wide lock.
 struct DeviceState {
-    bool ready = false;
+    std::atomic<bool> ready{false};
     int cus = 0;
     uint32_t* tables[2][kNumLaneChoices] = {};  // [algo][lane choice] compact operator images
     uint32_t* xinv[2] = {};       // [algo] x^(-8k), k = 0..127: removes the plan's zero padding
+    std::shared_mutex maps_mu;    // guards xtab and scratch
     std::map<uint64_t, uint32_t*> xtab;  // (algo, CH) -> x^(8*CH) operator for the plan's combine
     std::map<hipStream_t, std::unique_ptr<StreamScratch>> scratch;
 };
 
-std::mutex g_mu;
+std::mutex g_mu;  // device initialisation only
 DeviceState g_dev[kMaxDevices];
 std::atomic<int> g_forced_lanes{0};
 std::atomic<int> g_plan_mode{0};  // 0 auto, 1 direct (one entry per group), 2 chunked plan
@@ -233,7 +239,7 @@ struct DeviceScope {
 
 int init_device_locked(int dev) {
     DeviceState& ds = g_dev[dev];
-    if (ds.ready) return BKD_OK;
+    if (ds.ready.load(std::memory_order_acquire)) return BKD_OK;
     int prev = 0;
     BKD_HIP(hipGetDevice(&prev));
     BKD_HIP(hipSetDevice(dev));
@@ -263,14 +269,22 @@ int init_device_locked(int dev) {
         (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
     }
     BKD_HIP(hipSetDevice(prev));
-    ds.ready = true;
+    ds.ready.store(true, std::memory_order_release);
     return BKD_OK;
 }
 
 // x^(8*ch) operator tables for the plan's combine, built once per (algo, ch) and device.
 int xtab_for(DeviceState& ds, int algo, uint32_t ch, const uint32_t** out) {
-    std::lock_guard<std::mutex> lk(g_mu);
     const uint64_t key = ((uint64_t)algo << 32) | ch;
+    {
+        std::shared_lock<std::shared_mutex> rd(ds.maps_mu);
+        auto it = ds.xtab.find(key);
+        if (it != ds.xtab.end()) {
+            *out = it->second;
+            return BKD_OK;
+        }
+    }
+    std::unique_lock<std::shared_mutex> wr(ds.maps_mu);
     auto it = ds.xtab.find(key);
     if (it == ds.xtab.end()) {
         std::vector<uint32_t> xt(1024);
@@ -294,7 +308,7 @@ int enter(hipStream_t st, DeviceScope& scope, DeviceState** out) {
         BKD_HIP(hipSetDevice(dev));
         scope.prev = cur;
     }
-    {
+    if (!g_dev[dev].ready.load(std::memory_order_acquire)) {  // first call on the device only
         std::lock_guard<std::mutex> lk(g_mu);
         rc = init_device_locked(dev);
     }
@@ -303,8 +317,16 @@ int enter(hipStream_t st, DeviceScope& scope, DeviceState** out) {
     return BKD_OK;
 }
 
+// The stream's scratch, or nullptr when nothing was ever enqueued on it (no entry is created).
+StreamScratch* scratch_find(DeviceState& ds, hipStream_t st) {
+    std::shared_lock<std::shared_mutex> rd(ds.maps_mu);
+    auto it = ds.scratch.find(st);
+    return it == ds.scratch.end() ? nullptr : it->second.get();
+}
+
 StreamScratch& scratch_for(DeviceState& ds, hipStream_t st) {
-    std::lock_guard<std::mutex> lk(g_mu);
+    if (StreamScratch* sc = scratch_find(ds, st)) return *sc;  // hits take the shared lock only
+    std::unique_lock<std::shared_mutex> wr(ds.maps_mu);
     auto& slot = ds.scratch[st];
     if (!slot) slot.reset(new StreamScratch());
     return *slot;
@@ -491,10 +513,13 @@ bool indexed_direct(uint64_t size) {
     return mode == 1 || (mode == 0 && size <= kDirectMaxBytes) || size >= bkd::kPlanMaxSize;
 }
 
+// route: -1 decided here from the plan mode and the buffer size, else the caller's decision
+// (0 direct, 1 plan) so that a route chosen once per call cannot change under bkd_set_plan_mode.
 int indexed_batch(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, const uint64_t* offsets,
                   const uint32_t* lengths, uint64_t n, const uint32_t* seeds, uint32_t seed_all, uint32_t* out,
-                  hipStream_t st, const uint32_t* ext_flag, uint32_t ext_epoch) {
-    if (!indexed_direct(size))
+                  hipStream_t st, const uint32_t* ext_flag, uint32_t ext_epoch, int route) {
+    if (route < 0) route = indexed_direct(size) ? 0 : 1;
+    if (route == 1)
         return launch_plan(ds, algo, base, size, offsets, lengths, n, seeds, seed_all, out, st, true, true, ext_flag,
                            ext_epoch);
     uint32_t* err = nullptr;
@@ -542,26 +567,49 @@ struct HostStage {
     uint32_t* d_res[2] = {};
     hipStream_t st[2] = {};
     hipEvent_t done[2] = {};
-    // framed-entry batches (bkd_digest_*_batch_host), allocated on first use: per-entry ids, LACs
-    // and length fields in (24 B per entry), frame headers and first_bad out
+    // framed-entry batches (bkd_digest_*_batch_host), allocated on first use and sized per path
+    // (ADVICE r2): package needs per-entry ids, LACs and length fields in (24 B per entry) and the
+    // frame headers out; verify only its first_bad word
     static constexpr size_t kAux = 64u << 20;
-    bool aux_ready = false;
+    bool pkg_ready = false, fb_ready = false;
     uint8_t* h_aux[2] = {};
     uint8_t* d_aux[2] = {};
     uint8_t* h_frm[2] = {};
     uint8_t* d_frm[2] = {};
+    uint64_t* h_fb[2] = {};
+    uint64_t* d_fb[2] = {};
     // (each allocation is made once: a call after a failed init completes the set, nothing leaks)
-    // (each allocation is made once: a call after a failed init completes the set, nothing leaks)
-    int init_aux() {
-        if (aux_ready) return BKD_OK;
+    int init_package() {
+        if (pkg_ready) return BKD_OK;
         for (int s = 0; s < 2; ++s) {
             if (!h_aux[s]) BKD_HIP(hipHostMalloc((void**)&h_aux[s], kAux, hipHostMallocDefault));
             if (!d_aux[s]) BKD_HIP(hipMalloc((void**)&d_aux[s], kAux));
             if (!h_frm[s]) BKD_HIP(hipHostMalloc((void**)&h_frm[s], kAux, hipHostMallocDefault));
             if (!d_frm[s]) BKD_HIP(hipMalloc((void**)&d_frm[s], kAux));
         }
-        aux_ready = true;
+        pkg_ready = true;
         return BKD_OK;
+    }
+    int init_verify() {
+        if (fb_ready) return BKD_OK;
+        for (int s = 0; s < 2; ++s) {
+            if (!h_fb[s]) BKD_HIP(hipHostMalloc((void**)&h_fb[s], sizeof(uint64_t), hipHostMallocDefault));
+            if (!d_fb[s]) BKD_HIP(hipMalloc((void**)&d_fb[s], sizeof(uint64_t)));
+        }
+        fb_ready = true;
+        return BKD_OK;
+    }
+    ~HostStage() {  // (bkd_host_release: idle sets only, so no work of theirs is queued)
+        for (int s = 0; s < 2; ++s) {
+            for (void* h : {(void*)h_pin[s], (void*)h_off[s], (void*)h_len[s], (void*)h_seed[s], (void*)h_res[s],
+                            (void*)h_aux[s], (void*)h_frm[s], (void*)h_fb[s]})
+                if (h) (void)hipHostFree(h);
+            for (void* d : {(void*)d_buf[s], (void*)d_off[s], (void*)d_len[s], (void*)d_seed[s], (void*)d_res[s],
+                            (void*)d_aux[s], (void*)d_frm[s], (void*)d_fb[s]})
+                if (d) (void)hipFree(d);
+            if (st[s]) (void)hipStreamDestroy(st[s]);
+            if (done[s]) (void)hipEventDestroy(done[s]);
+        }
     }
     int init() {
         if (ready) return BKD_OK;
@@ -633,77 +681,17 @@ class StageLease {
     HostStage* hs_ = nullptr;
 };
 
-// Host threads for the copies into pinned staging (a pageable source, or a list of separate
-// entry buffers such as a ByteBufList): one core copies ~10-20 GB/s, below PCIe Gen5's ~55.
-class CopyPool {
-  public:
-    static CopyPool& get() {
-        static CopyPool pool;
-        return pool;
-    }
-    // Runs f(part) for part = 0..parts-1 (part 0 on the calling thread) and waits for all.
-    void run(int parts, const std::function<void(int)>& f) {
-        parts = std::max(1, std::min(parts, (int)workers_.size() + 1));
-        if (parts == 1) return f(0);
-        std::unique_lock<std::mutex> call(call_mu_);  // one parallel copy at a time
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            job_ = &f;
-            parts_ = parts;
-            pending_ = parts - 1;
-            ++gen_;
-        }
-        cv_.notify_all();
-        f(0);
-        std::unique_lock<std::mutex> lk(mu_);
-        done_.wait(lk, [&] { return pending_ == 0; });
-        job_ = nullptr;
-    }
-    int threads() const { return (int)workers_.size() + 1; }
-    ~CopyPool() {
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        for (auto& t : workers_) t.join();
-    }
-
-  private:
-    CopyPool() {
-        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-        // 8 (BKD_COPY_THREADS overrides): 12 measured no better on the 16-core share of the GPU box
-        // (host verify of 1M separate 4 KiB frames 42.5 vs 43.4 GiB/s mean, 33-51 run to run)
-        unsigned want = std::min(8u, std::max(1u, hw / 2));
-        if (const char* v = getenv("BKD_COPY_THREADS")) want = std::max(1u, std::min(64u, (unsigned)atoi(v)));
-        const int n = (int)want - 1;
-        for (int w = 0; w < n; ++w) workers_.emplace_back([this, w] { loop(w + 1); });
-    }
-    void loop(int part) {
-        uint64_t seen = 0;
-        for (;;) {
-            const std::function<void(int)>* f = nullptr;
-            {
-                std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-                if (stop_) return;
-                seen = gen_;
-                if (part >= parts_) continue;
-                f = job_;
-            }
-            (*f)(part);
-            std::lock_guard<std::mutex> lk(mu_);
-            if (--pending_ == 0) done_.notify_all();
-        }
-    }
-    std::vector<std::thread> workers_;
-    std::mutex mu_, call_mu_;
-    std::condition_variable cv_, done_;
-    const std::function<void(int)>* job_ = nullptr;
-    int parts_ = 0, pending_ = 0;
-    uint64_t gen_ = 0;
-    bool stop_ = false;
-};
+// Host copies into pinned staging (a pageable source, or a list of separate entry buffers such as a
+// ByteBufList) run on the library's host pool (host_batch.hpp): one core copies ~10-20 GB/s, below
+// PCIe Gen5's ~55. At most BKD_COPY_THREADS parts (default 8: 12 measured no better on the 16-core
+// share of the GPU box, host verify of 1M separate 4 KiB frames 42.5 vs 43.4 GiB/s mean).
+int copy_threads() {
+    static const int t = [] {
+        const char* v = getenv("BKD_COPY_THREADS");
+        return v ? std::max(1, std::min(64, atoi(v))) : 8;
+    }();
+    return std::min(t, bkd::host::Pool::get().active());
+}
 
 // Bytes per copy-pool part (BKD_COPY_PART_KIB overrides the default).
 size_t copy_part_bytes() {
@@ -717,8 +705,8 @@ size_t copy_part_bytes() {
 
 // memcpy of one range on the copy pool (parts of >= copy_part_bytes()).
 void parallel_copy(uint8_t* dst, const uint8_t* src, size_t n) {
-    CopyPool& pool = CopyPool::get();
-    const int parts = (int)std::min<size_t>((size_t)pool.threads(), std::max<size_t>(1, n / copy_part_bytes()));
+    bkd::host::Pool& pool = bkd::host::Pool::get();
+    const int parts = (int)std::min<size_t>((size_t)copy_threads(), std::max<size_t>(1, n / copy_part_bytes()));
     const size_t per = (n + parts - 1) / parts;
     pool.run(parts, [&](int p) {
         const size_t a = std::min(n, per * (size_t)p), b = std::min(n, a + per);
@@ -734,8 +722,8 @@ void gather_entries(const void* const* src, const uint32_t* len, uint64_t cnt, u
         off[i] = at;
         at += len[i];
     }
-    CopyPool& pool = CopyPool::get();
-    const int parts = (int)std::min<uint64_t>((uint64_t)pool.threads(), std::max<uint64_t>(1, at / copy_part_bytes()));
+    bkd::host::Pool& pool = bkd::host::Pool::get();
+    const int parts = (int)std::min<uint64_t>((uint64_t)copy_threads(), std::max<uint64_t>(1, at / copy_part_bytes()));
     const uint64_t per = (at + parts - 1) / parts;
     pool.run(parts, [&](int p) {
         // entries whose first byte lies in [p*per, (p+1)*per)
@@ -748,7 +736,7 @@ void gather_entries(const void* const* src, const uint32_t* len, uint64_t cnt, u
 
 int indexed_batch(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, const uint64_t* offsets,
                   const uint32_t* lengths, uint64_t n, const uint32_t* seeds, uint32_t seed_all, uint32_t* out,
-                  hipStream_t st, const uint32_t* ext_flag = nullptr, uint32_t ext_epoch = 0);
+                  hipStream_t st, const uint32_t* ext_flag = nullptr, uint32_t ext_epoch = 0, int route = -1);
 
 bool is_pinned_host(const void* p) {
     hipPointerAttribute_t attr;
@@ -943,8 +931,11 @@ int verify_framed(DeviceState& ds, hipStream_t st, int algo, int64_t ledger_id, 
     // ones keep the three-kernel sequence)
     // — and, as the plan's own near-uniform gate, only where one frame per group uses the plan's lane
     // count: a few huge frames need the plan's chunks to fill the chip
+    // the payloads' route, decided once for the whole call (a second read of the plan mode
+    // could send them to the direct kernel, which ignores the gate, after the fused kernel ran)
+    const int route = indexed_direct(framed_size) ? 0 : 1;
     const int fused_lanes = auto_lanes(framed_size / n, n, ds.cus);
-    const bool fused = BKD_VERIFY_FUSED && !indexed_direct(framed_size) && fused_lanes == g_plan_lanes.load();
+    const bool fused = BKD_VERIFY_FUSED && route == 1 && fused_lanes == g_plan_lanes.load();
     uint32_t* vflag = nullptr;
     uint32_t vepoch = 0;
     if (fused) {
@@ -980,7 +971,7 @@ int verify_framed(DeviceState& ds, hipStream_t st, int algo, int64_t ledger_id, 
     if (e != hipSuccess) return fail(BKD_ERR_HIP, hipGetErrorString(e));
     // payload CRCs land in d_status, then verify_finish turns them into status codes
     int rc = indexed_batch(ds, algo, (const uint8_t*)d_framed, framed_size, poff, plen, n, seeds, 0,
-                           reinterpret_cast<uint32_t*>(d_status), st, vflag, vepoch);
+                           reinterpret_cast<uint32_t*>(d_status), st, vflag, vepoch, route);
     if (rc) return rc;
     hipLaunchKernelGGL(bkd::verify_finish_kernel, dim3(blocks), dim3(256), 0, st, expect, pre, n, d_status,
                        (unsigned long long*)d_first_bad, vflag, vepoch);
@@ -1005,6 +996,10 @@ int host_segments(HostStage& hs, const uint32_t* h_lengths, uint64_t n, uint64_t
         busy[s] = false;
         return drain_slot(s, pend_i0[s], pend_cnt[s]);
     };
+    // every entry fits a segment, checked before any work is enqueued
+    for (uint64_t i = 0; i < n; ++i)
+        if (h_lengths[i] > HostStage::kSeg)
+            return fail(BKD_ERR_INVALID_ARG, "host entry " + std::to_string(i) + " is larger than 64 MiB");
     int rc = BKD_OK;
     uint64_t i0 = 0;
     for (int k = 0; i0 < n && rc == BKD_OK; ++k) {
@@ -1012,10 +1007,19 @@ int host_segments(HostStage& hs, const uint32_t* h_lengths, uint64_t n, uint64_t
         uint64_t i1 = i0, bytes = 0;
         while (i1 < n && i1 - i0 < max_entries && (i1 == i0 || bytes + h_lengths[i1] <= HostStage::kSeg))
             bytes += h_lengths[i1++];
-        if (bytes > HostStage::kSeg) return fail(BKD_ERR_INVALID_ARG, "a host entry is larger than 64 MiB");
         if ((rc = drain(s))) break;
-        if ((rc = seg(s, i0, i1 - i0, bytes))) break;
-        BKD_HIP(hipEventRecord(hs.done[s], hs.st[s]));
+        if ((rc = seg(s, i0, i1 - i0, bytes))) {
+            (void)hipStreamSynchronize(hs.st[s]);  // copies of the failed segment may be queued
+            break;
+        }
+        // every exit below goes through the final drains: no staging set returns to the pool with
+        // copies or kernels of this call still queued on its streams
+        const hipError_t e = hipEventRecord(hs.done[s], hs.st[s]);
+        if (e != hipSuccess) {
+            rc = fail(BKD_ERR_HIP, std::string("hipEventRecord: ") + hipGetErrorString(e));
+            (void)hipStreamSynchronize(hs.st[s]);
+            break;
+        }
         busy[s] = true;
         pend_i0[s] = i0;
         pend_cnt[s] = i1 - i0;
@@ -1041,6 +1045,32 @@ uint64_t cpu_route_max() {
 // Per-call resumes longer than this run as consecutive pieces, each resuming from the last
 // (entry lengths are 32-bit in the batch kernels).
 constexpr uint64_t kResumePiece = 1ull << 31;
+
+// Route of the host-resident batches (bkd_crc_batch_host, bkd_digest_*_batch_host): 0 automatic,
+// 1 CPU (host_batch.cpp over the host pool), 2 GPU (pinned staging, PCIe, the device sequence).
+std::atomic<int> g_host_route{0};
+
+// The automatic choice, from the measured crossover (profiles/r03_host_route.log): a
+// host-resident batch through the GPU is bound by PCIe (~51 GiB/s) and, for separate entry buffers,
+// by the host gather into pinned staging, which costs the cores as much as folding the bytes; the
+// CPU route scales with the cores. BKD_HOST_ROUTE_MIN_THREADS overrides the crossover.
+int cpu_route_min_threads() {
+    static const int t = [] {
+        if (const char* v = getenv("BKD_HOST_ROUTE_MIN_THREADS")) return std::max(1, atoi(v));
+        return bkd::host::has_wide_fold() ? 2 : 4;
+    }();
+    return t;
+}
+
+// 1 = CPU, 2 = GPU, < 0 = error (a GPU route forced without a device).
+int host_route() {
+    const int r = g_host_route.load(std::memory_order_relaxed);
+    if (r == 1) return 1;
+    if (visible_devices() <= 0)  // the provider never fails for lack of a device
+        return r == 2 ? fail(BKD_ERR_NO_DEVICE, "no HIP device (host batch route forced to the GPU)") : 1;
+    if (r == 2) return 2;
+    return bkd::host::Pool::get().active() >= cpu_route_min_threads() ? 1 : 2;
+}
 
 int cpu_resume(int algo, uint32_t current, const void* p, uint64_t len, uint32_t* out) {
     *out = ~bkd::host::crc_raw(algo, ~current, (const uint8_t*)p, (size_t)len);
@@ -1225,7 +1255,12 @@ int bkd_stream_sync(void* stream) {
     DeviceState* ds = nullptr;
     int rc = enter(st, scope, &ds);
     if (rc) return rc;
-    StreamScratch& sc = scratch_for(*ds, st);
+    StreamScratch* scp = scratch_find(*ds, st);  // (no entry for streams that only sync)
+    if (!scp) {
+        BKD_HIP(hipStreamSynchronize(st));
+        return BKD_OK;
+    }
+    StreamScratch& sc = *scp;
     std::lock_guard<std::recursive_mutex> lk(sc.mu);
     if (!sc.err) {  // nothing indexed was ever enqueued on this stream
         BKD_HIP(hipStreamSynchronize(st));
@@ -1247,7 +1282,7 @@ int bkd_stream_release(void* stream) {
     if (rc) return rc;
     std::unique_ptr<StreamScratch> sc;
     {
-        std::lock_guard<std::mutex> lk(g_mu);
+        std::unique_lock<std::shared_mutex> wr(ds->maps_mu);
         auto it = ds->scratch.find(st);
         if (it == ds->scratch.end()) {
             BKD_HIP(hipStreamSynchronize(st));
@@ -1286,6 +1321,12 @@ int bkd_crc_batch_host(int algo, const void* h_base, uint64_t base_size, const u
         if (h_offsets[i] > base_size || (uint64_t)h_lengths[i] > base_size - h_offsets[i])
             return fail(BKD_ERR_BOUNDS, "entry " + std::to_string(i) + " exceeds base buffer");
         if (i && h_offsets[i] < h_offsets[i - 1]) sorted = false;
+    }
+    const int route = host_route();
+    if (route < 0) return route;
+    if (route == 1) {
+        bkd::host::crc_indexed(algo, (const uint8_t*)h_base, h_offsets, h_lengths, n, h_seeds, seed_all, h_out);
+        return BKD_OK;
     }
     DeviceScope scope;
     DeviceState* ds = nullptr;
@@ -1406,6 +1447,53 @@ uint64_t bkd_get_cpu_route_max(void) { return cpu_route_max(); }
 
 const char* bkd_cpu_impl(void) { return bkd::host::impl_name(); }
 
+int bkd_set_host_batch_route(int route) {
+    if (route < 0 || route > 2) return fail(BKD_ERR_INVALID_ARG, "host batch route must be 0 (auto), 1 (CPU) or 2 (GPU)");
+    g_host_route.store(route);
+    return BKD_OK;
+}
+
+int bkd_get_host_batch_route(void) {
+    const int r = host_route();
+    return r < 0 ? 2 : r;
+}
+
+int bkd_set_host_threads(int threads) {
+    if (threads < 0) return fail(BKD_ERR_INVALID_ARG, "threads must be >= 0");
+    bkd::host::Pool::get().set_active(threads);
+    return BKD_OK;
+}
+
+int bkd_get_host_threads(void) { return bkd::host::Pool::get().active(); }
+
+int bkd_host_release(void) {
+    for (int d = 0; d < kMaxDevices; ++d) {
+        StagePool& pool = g_stages[d];
+        std::vector<std::unique_ptr<HostStage>> gone;
+        {
+            std::lock_guard<std::mutex> lk(pool.mu);
+            for (HostStage* hs : pool.idle) {
+                auto it = std::find_if(pool.all.begin(), pool.all.end(),
+                                       [&](const std::unique_ptr<HostStage>& p) { return p.get() == hs; });
+                if (it != pool.all.end()) {
+                    gone.push_back(std::move(*it));
+                    pool.all.erase(it);
+                }
+            }
+            pool.idle.clear();
+        }
+        if (!gone.empty()) {
+            int prev = 0;
+            if (hipGetDevice(&prev) == hipSuccess && hipSetDevice(d) == hipSuccess) {
+                gone.clear();  // frees the pinned and device buffers, streams and events
+                (void)hipSetDevice(prev);
+            }
+        }
+        pool.cv.notify_all();  // callers waiting for a set may create one again
+    }
+    return BKD_OK;
+}
+
 int bkd_digest_package_batch(int algo, int64_t ledger_id, const int64_t* d_entry_ids, const int64_t* d_lacs,
                              const int64_t* d_length_fields, const void* d_payload, uint64_t payload_size,
                              const uint64_t* d_offsets, const uint32_t* d_lengths, uint64_t n, void* d_frames,
@@ -1452,13 +1540,20 @@ int bkd_digest_verify_batch_host(int algo, int64_t ledger_id, int64_t first_entr
     if (!h_frames || !h_lengths || !h_status) return fail(BKD_ERR_INVALID_ARG, "null buffer");
     for (uint64_t i = 0; i < n; ++i)
         if (h_lengths[i] && !h_frames[i]) return fail(BKD_ERR_INVALID_ARG, "null frame " + std::to_string(i));
+    const int route = host_route();
+    if (route < 0) return route;
+    if (route == 1) {
+        *h_first_bad = bkd::host::verify_frames(algo, ledger_id, first_entry_id, skip_entry_check ? 1 : 0,
+                                                (const uint8_t* const*)h_frames, h_lengths, n, h_status);
+        return BKD_OK;
+    }
     DeviceScope scope;
     DeviceState* ds = nullptr;
     int rc = enter(nullptr, scope, &ds);
     if (rc) return rc;
     StageLease lease((int)(ds - g_dev));
     HostStage& hs = *lease;
-    if ((rc = hs.init()) || (rc = hs.init_aux())) return rc;
+    if ((rc = hs.init()) || (rc = hs.init_verify())) return rc;
     const int id_checks = skip_entry_check ? 1 : 0;
     auto seg = [&](int s, uint64_t i0, uint64_t cnt, uint64_t bytes) -> int {
         gather_entries(h_frames + i0, h_lengths + i0, cnt, hs.h_pin[s], hs.h_off[s]);
@@ -1466,17 +1561,17 @@ int bkd_digest_verify_batch_host(int algo, int64_t ledger_id, int64_t first_entr
         BKD_HIP(hipMemcpyAsync(hs.d_buf[s], hs.h_pin[s], bytes, hipMemcpyHostToDevice, st));
         BKD_HIP(hipMemcpyAsync(hs.d_off[s], hs.h_off[s], cnt * 8, hipMemcpyHostToDevice, st));
         BKD_HIP(hipMemcpyAsync(hs.d_len[s], h_lengths + i0, cnt * 4, hipMemcpyHostToDevice, st));
-        uint64_t* d_fb = reinterpret_cast<uint64_t*>(hs.d_frm[s]);
+        uint64_t* d_fb = hs.d_fb[s];
         int r = verify_framed(*ds, st, algo, ledger_id, first_entry_id + (int64_t)i0, id_checks, hs.d_buf[s], bytes,
                               hs.d_off[s], hs.d_len[s], cnt, reinterpret_cast<int32_t*>(hs.d_res[s]), d_fb);
         if (r) return r;
         BKD_HIP(hipMemcpyAsync(hs.h_res[s], hs.d_res[s], cnt * 4, hipMemcpyDeviceToHost, st));
-        BKD_HIP(hipMemcpyAsync(hs.h_frm[s], d_fb, 8, hipMemcpyDeviceToHost, st));
+        BKD_HIP(hipMemcpyAsync(hs.h_fb[s], d_fb, 8, hipMemcpyDeviceToHost, st));
         return BKD_OK;
     };
     auto drain = [&](int s, uint64_t i0, uint64_t cnt) -> int {
         memcpy(h_status + i0, hs.h_res[s], cnt * 4);
-        const uint64_t fb = *reinterpret_cast<const uint64_t*>(hs.h_frm[s]);
+        const uint64_t fb = *hs.h_fb[s];
         if (fb < cnt && i0 + fb < *h_first_bad) *h_first_bad = i0 + fb;
         return BKD_OK;
     };
@@ -1496,13 +1591,21 @@ int bkd_digest_package_batch_host(int algo, int64_t ledger_id, const int64_t* h_
         return fail(BKD_ERR_INVALID_ARG, "frame_stride must be in [32 + digest length, 4096]");
     for (uint64_t i = 0; i < n; ++i)
         if (h_lengths[i] && !h_payloads[i]) return fail(BKD_ERR_INVALID_ARG, "null payload " + std::to_string(i));
+    const int route = host_route();
+    if (route < 0) return route;
+    if (route == 1) {
+        bkd::host::package_frames(algo, ledger_id, h_entry_ids, h_lacs, h_length_fields,
+                                  (const uint8_t* const*)h_payloads, h_lengths, n, (uint8_t*)h_frames, frame_stride,
+                                  h_digests);
+        return BKD_OK;
+    }
     DeviceScope scope;
     DeviceState* ds = nullptr;
     int rc = enter(nullptr, scope, &ds);
     if (rc) return rc;
     StageLease lease((int)(ds - g_dev));
     HostStage& hs = *lease;
-    if ((rc = hs.init()) || (rc = hs.init_aux())) return rc;
+    if ((rc = hs.init()) || (rc = hs.init_package())) return rc;
     const uint64_t max_entries = std::min<uint64_t>(HostStage::kSegEntries, HostStage::kAux / frame_stride);
     auto seg = [&](int s, uint64_t i0, uint64_t cnt, uint64_t bytes) -> int {
         gather_entries(h_payloads + i0, h_lengths + i0, cnt, hs.h_pin[s], hs.h_off[s]);

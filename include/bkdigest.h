@@ -23,8 +23,10 @@
  * caller's HIP stream (hipStream_t passed as void*, NULL = the null stream) and run on that
  * stream's device (the calling thread's current device for the null stream); buffers are
  * borrowed only until the stream reaches the end of the call's work.
- * Batch entry points always run on the GPU (BKD_ERR_NO_DEVICE without one). The per-call
- * host-buffer resumes (bkd_resume / bkd_resume_host) take the library's own CPU route for
+ * Device-resident batch entry points always run on the GPU (BKD_ERR_NO_DEVICE without one).
+ * Host-resident batches (bkd_crc_batch_host, bkd_digest_*_batch_host) take the GPU through pinned
+ * staging or the library's own threaded CPU route, by the measured crossover (bkd_set_host_batch_route).
+ * The per-call host-buffer resumes (bkd_resume / bkd_resume_host) take the CPU route for
  * buffers up to bkd_get_cpu_route_max() bytes and whenever no device is visible, so the
  * provider never fails for lack of a GPU, as the reference's class-init selection never does
  * ($CJ/checksum/Crc32cIntChecksum.java:28-36).
@@ -39,7 +41,7 @@
 extern "C" {
 #endif
 
-#define BKD_ABI_VERSION 3
+#define BKD_ABI_VERSION 4
 
 /* only the entry points below are exported (the library is built with -fvisibility=hidden) */
 #ifndef BKD_API
@@ -126,11 +128,28 @@ BKD_API int bkd_stream_sync(void* stream);
 BKD_API int bkd_stream_release(void* stream);
 
 /* ---- host-resident batches (the end-to-end path: Netty buffers in, digests out) -------
- * Synchronous. Copies the payload through pinned staging buffers with hipMemcpyAsync
- * (double-buffered H2D -> kernel -> D2H). Same semantics as bkd_crc_batch. */
+ * Synchronous. Same semantics as bkd_crc_batch (bounds checked on the host: BKD_ERR_BOUNDS before
+ * any work). GPU route: the payload goes through pinned staging buffers with hipMemcpyAsync
+ * (double-buffered H2D -> kernel -> D2H). CPU route: one fold per entry on the library's host
+ * threads (host_batch.cpp). */
 BKD_API int bkd_crc_batch_host(int algo, const void* h_base, uint64_t base_size, const uint64_t* h_offsets,
                        const uint32_t* h_lengths, uint64_t n, const uint32_t* h_seeds, uint32_t seed_all,
                        uint32_t* h_out);
+/* Route of the host-resident batches: 0 = automatic (the CPU route when at least the measured
+ * crossover's number of host threads is available: a batch that starts in host memory is bound by
+ * PCIe and the host gather through the GPU; the CPU route also whenever no device is
+ * visible), 1 = always the CPU route, 2 = always the GPU (BKD_ERR_NO_DEVICE without one).
+ * get: the route the next host-resident batch takes (1 or 2). The reference verifies these entries
+ * one crc32c() call at a time on its caller's thread ($BK/client/BatchedReadOp.java:164-190). */
+BKD_API int bkd_set_host_batch_route(int route);
+BKD_API int bkd_get_host_batch_route(void);
+/* Host threads the CPU route and the staging copies may use (0 = all of the pool: BKD_HOST_THREADS,
+ * else the cores this process may run on, capped by a cgroup CPU quota). */
+BKD_API int bkd_set_host_threads(int threads);
+BKD_API int bkd_get_host_threads(void);
+/* Frees the idle pinned staging sets of the GPU route (host and device memory, streams); sets in use
+ * by a running call are kept. A later host-resident batch through the GPU creates them again. */
+BKD_API int bkd_host_release(void);
 
 /* ---- per-call drop-in (IntHash.resume) ---------------------------------------------------
  * resume(current, ptr, len) for ONE buffer, synchronous. Replaces Sse42Crc32C.nativeUnsafe /
@@ -198,9 +217,10 @@ BKD_API int bkd_digest_verify_batch(int algo, int64_t ledger_id, int64_t first_e
 /* Host-resident framed batches (SURVEY §8f rows 1-2 with the entries in host memory, BASELINE
  * config 5): entry i is its own host buffer h_frames[i] / h_payloads[i] of h_lengths[i] bytes,
  * as BatchedReadOp's ByteBufList ($BK/client/BatchedReadOp.java:164-190) and PendingAddOp's
- * payloads ($BK/client/PendingAddOp.java:261) hold them. The library gathers them into pinned
- * staging (segments of <= 64 MiB, double-buffered, host copies on a thread pool), copies H2D,
- * runs the device sequence of the device-resident call and copies the results back. Synchronous.
+ * payloads ($BK/client/PendingAddOp.java:261) hold them. Route as bkd_crc_batch_host: GPU = the
+ * library gathers them into pinned staging (segments of <= 64 MiB, double-buffered, host copies on
+ * a thread pool), copies H2D, runs the device sequence of the device-resident call and copies the
+ * results back; CPU = DigestManager's per-entry arithmetic on the host threads. Synchronous.
  * verify: h_status[i] and *h_first_bad as bkd_digest_verify_batch (n if all verified).
  * package: writes frame i's [32 B header][digest] to h_frames + i*frame_stride
  * (32 + mac <= frame_stride <= 4096) and the digest value to h_digests[i]. */

@@ -120,6 +120,9 @@ def ref():
                                                ctypes.c_int, ctypes.c_int, _u32p]
         L.ref_crc32c_batch_timed.restype = ctypes.c_double
         L.ref_crc32c_batch_timed.argtypes = [_u8p, _u64p, _u32p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, _u32p]
+        L.ref_verify_frames_timed.restype = ctypes.c_double
+        L.ref_verify_frames_timed.argtypes = [ctypes.c_void_p, _u32p, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64,
+                                              ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int32)]
         _ref = L
     return _ref
 

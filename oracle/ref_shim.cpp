@@ -107,4 +107,58 @@ double ref_crc32c_batch_timed(const uint8_t* base, const uint64_t* offsets, cons
     return std::chrono::duration<double>(t1 - t0).count();
 }
 
+// BatchedReadOp's verify loop over a ByteBufList in host memory ($BK/client/BatchedReadOp.java:164-190),
+// CRC32C: per frame DigestManager.verifyDigest's two updates through circe (update(0, [0, 32)) then
+// update(digest, [36, len)), DigestManager.java:236-239) and the compare with getInt(32) (:241-249),
+// then the ledger / entry id checks (:264-281). Frames split into ranges of about equal bytes over
+// `threads` std::threads; `reps` passes. status[i] as bkd_digest_verify_batch_host (0 ok, 1 too
+// short, 2 digest, 3 ledger id, 4 entry id). Returns wall seconds for all passes.
+double ref_verify_frames_timed(const uint8_t* const* frames, const uint32_t* lengths, uint64_t n, int64_t ledger_id,
+                               int64_t first_entry_id, int threads, int reps, int32_t* status) {
+    crc32c_initialize();
+    const chunk_config* cfg = &default_config();
+    if (threads < 1) threads = 1;
+    std::vector<uint64_t> cut(threads + 1, n);
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; ++i) total += lengths[i];
+    cut[0] = 0;
+    uint64_t acc = 0;
+    int t = 1;
+    for (uint64_t i = 0; i < n && t < threads; ++i) {
+        acc += lengths[i];
+        while (t < threads && acc * threads >= total * t) cut[t++] = i + 1;
+    }
+    auto be = [](const uint8_t* p, int k) {
+        uint64_t v = 0;
+        for (int b = 0; b < k; ++b) v = (v << 8) | p[b];
+        return v;
+    };
+    auto t0 = std::chrono::steady_clock::now();
+    for (int r = 0; r < reps; ++r) {
+        std::vector<std::thread> pool;
+        for (int k = 0; k < threads; ++k) {
+            const uint64_t lo = cut[k], hi = cut[k + 1];
+            pool.emplace_back([=]() {
+                for (uint64_t i = lo; i < hi; ++i) {
+                    const uint8_t* f = frames[i];
+                    const uint32_t l = lengths[i];
+                    if (l < 36u) {
+                        status[i] = 1;
+                        continue;
+                    }
+                    uint32_t d = crc32c(0, f, 32, cfg);
+                    d = crc32c(d, f + 36, l - 36u, cfg);
+                    if (d != (uint32_t)be(f + 32, 4)) status[i] = 2;
+                    else if ((int64_t)be(f, 8) != ledger_id) status[i] = 3;
+                    else if ((int64_t)be(f + 8, 8) != first_entry_id + (int64_t)i) status[i] = 4;
+                    else status[i] = 0;
+                }
+            });
+        }
+        for (auto& th : pool) th.join();
+    }
+    auto t1 = std::chrono::steady_clock::now();
+    return std::chrono::duration<double>(t1 - t0).count();
+}
+
 }  // extern "C"

@@ -29,4 +29,9 @@ def gpu():
     from bookkeeper_amd import _native
     assert _native.device_count() > 0
     torch.cuda.set_device(0)
+    # GPU tests exercise the GPU route of the host-resident batches (the automatic choice on a host
+    # with enough cores is the CPU route, which the CPU suite tests); tests of the automatic or CPU
+    # route select it explicitly (checksum.host_batch_route)
+    from bookkeeper_amd import checksum as ck
+    ck.set_host_batch_route(ck.HOST_ROUTE_GPU)
     return torch.device("cuda", 0)

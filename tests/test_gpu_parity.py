@@ -4,6 +4,7 @@ Bit-exact for every case (integer arithmetic). Mirrors the reference's own tests
 ChecksumTest.java:36-92 (KATs, resume, incremental), CRCTest.java:117-135 (check values),
 CompositeByteBufUnwrapBugReproduceTest (DigestManager framing with payload b[i] = (byte) i).
 """
+import os
 import zlib
 
 import numpy as np
@@ -596,10 +597,30 @@ def test_plan_length_sweep_packed(gpu, geom, shift):
         ck.set_plan_geometry()
 
 
-def test_zipf_full_size_plan_equals_direct(gpu):
-    """BASELINE config 3 at full size (1M Zipf entries, 6.8 GB): the chunked plan and the
-    one-entry-per-group kernel are independent decompositions and must agree on every entry; a
-    random sample of entries is also checked against the oracle."""
+def _threaded_reference(algo: int, host: np.ndarray, offs: np.ndarray, lens: np.ndarray) -> tuple[np.ndarray, str]:
+    """Every entry's digest from the reference side, threaded: CRC32C through the reference's own
+    circe crc32c() (oracle/_ref, crc32c_sse42.cpp:184-217), else the C oracle; CRC32 through zlib's
+    crc32() (= java.util.zip.CRC32, CRC32DigestManager.java:28-87)."""
+    n = offs.size
+    want = np.zeros(n, dtype=np.uint32)
+    o64 = np.ascontiguousarray(offs, dtype=np.uint64)
+    l32 = np.ascontiguousarray(lens, dtype=np.uint32)
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    args = (host.ctypes.data_as(oracle._u8p), o64.ctypes.data_as(oracle._u64p), l32.ctypes.data_as(oracle._u32p), n)
+    if algo == ck.CRC32C and oracle.ref() is not None:
+        oracle.ref().ref_crc32c_batch_timed(*args, threads, 1, want.ctypes.data_as(oracle._u32p))
+        return want, "reference circe crc32c()"
+    if algo == ck.CRC32:
+        oracle.lib().oracle_zlib_crc32_batch_timed(*args, threads, 1, want.ctypes.data_as(oracle._u32p))
+        return want, "zlib crc32()"
+    return oracle.batch(algo, host, offs, lens), "C oracle"
+
+
+def test_zipf_full_size_every_entry_vs_reference(gpu):
+    """BASELINE config 3 at full size (1M Zipf entries 64 B-64 KiB, 6.8 GB, packed, unaligned):
+    every digest through the automatic route (what bench.py --config zipf times), the chunked plan
+    and the one-entry-per-group kernel equals the reference's on the host copy of the same bytes —
+    CRC32C against circe crc32c() compiled from the reference, CRC32 against zlib."""
     import torch
     from bench import zipf_index
     offs, lens = zipf_index(1 << 20)
@@ -608,20 +629,17 @@ def test_zipf_full_size_plan_equals_direct(gpu):
     ck.fill_splitmix64(base, 42)
     d_off = torch.from_numpy(offs).to(gpu)
     d_len = torch.from_numpy(lens.astype(np.int32)).to(gpu)
-    rng = np.random.default_rng(3)
-    pick = np.sort(rng.choice(offs.size, 2000, replace=False))
-    for algo in (ck.CRC32C, ck.CRC32):
-        ck.set_plan_mode(2)
-        plan = ck.crc_batch(algo, base, d_off, d_len, sync_check=True).cpu().numpy().view(np.uint32)
-        ck.set_plan_mode(1)
-        direct = ck.crc_batch(algo, base, d_off, d_len, sync_check=True).cpu().numpy().view(np.uint32)
-        assert (plan == direct).all()
-        parts = [base[int(offs[i]):int(offs[i] + lens[i])].cpu().numpy() for i in pick]
-        host = np.concatenate(parts)
-        sub_offs = np.concatenate([[0], np.cumsum(lens[pick])[:-1]]).astype(np.int64)
-        want = oracle.batch(algo, host, sub_offs, lens[pick])
-        assert (plan[pick] == want).all()
-    ck.set_plan_mode(0)
+    host = base.cpu().numpy()
+    try:
+        for algo in (ck.CRC32C, ck.CRC32):
+            want, _ = _threaded_reference(algo, host, offs, lens)
+            for mode in (0, 2, 1):  # auto (the bench's route), chunked plan, direct
+                ck.set_plan_mode(mode)
+                got = ck.crc_batch(algo, base, d_off, d_len, sync_check=True).cpu().numpy().view(np.uint32)
+                bad = np.nonzero(got != want)[0]
+                assert bad.size == 0, (algo, mode, bad.size, bad[:5].tolist(), lens[bad[:5]].tolist())
+    finally:
+        ck.set_plan_mode(0)
 
 
 def test_concurrent_callers(gpu):

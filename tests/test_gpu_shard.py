@@ -134,3 +134,25 @@ def test_bench_self_launches_ranks(gpu):
     assert res["n_gpus"] == 2 and res["scaling"] == "weak"
     assert len(res["per_gpu"]) == 2 and all(p["GiB_s"] > 0 and p["solo_GiB_s"] > 0 for p in res["per_gpu"])
     assert 0 < res["efficiency_vs_solo"] < 2
+
+
+def test_bench_two_ranks_default_is_config4_shard(gpu):
+    """`bench.py --gpus N > 1` without --config measures config 4's per-GPU
+    workload (8M x 4 KiB = 32 GiB per rank, weak scaling). Rehearsed here with two gloo ranks on
+    this one card (2 x 32 GiB of HBM); the driver's N = 2/4/8 runs use nccl (= RCCL) for the same
+    three timing collectives."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--steps", "5",
+           "--warmup", "2", "--no-cpu-baseline"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert res["n_gpus"] == 2 and res["scaling"] == "weak"
+    assert res["config"]["entries_per_gpu"] == 8388608 and res["config"]["entry_bytes"] == 4096
+    assert res["config"]["workload"].startswith("config 4: 64M x 4 KiB over 8 GPUs, 8M per GPU")
+    assert len(res["per_gpu"]) == 2
+    for p in res["per_gpu"]:
+        assert p["GiB_s"] > 0 and p["solo_GiB_s"] > 0 and p["kernel_ms"] > 0
+    # whole-job value = both ranks' payload over the slowest rank's time
+    total = 2 * 8388608 * 4096 * res["steps"] / (1 << 30)
+    assert abs(res["value"] - total / (res["ms_per_step"] * res["steps"] / 1e3)) / res["value"] < 0.01

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     assert set(declared) <= exported
     # nothing but the declared entry points leaks as a C symbol (C++ kernel stubs are mangled)
     assert {x for x in exported if not x.startswith("_Z") and not x.startswith("__hip")} == set(declared)
-    assert L.bkd_abi_version() == 3  # 3: bkd_stream_release
+    assert L.bkd_abi_version() == 4  # 3: bkd_stream_release; 4: host batch routes, bkd_host_release
 
 
 def test_library_contains_gfx950_code():
@@ -37,8 +37,9 @@ def test_library_contains_gfx950_code():
 
 
 def test_no_device_per_call_takes_cpu_route_batches_fail_loudly():
-    """Crc32cIntChecksum.java:28-36 never throws: with no device the per-call resume is served by the
-    library's own CPU route; batch entry points still refuse to run (no silent CPU batch path)."""
+    """Crc32cIntChecksum.java:28-36 never throws: with no device the per-call resume and the
+    host-resident batches are served by the library's own CPU route; device-resident batches and a
+    host batch forced onto the GPU refuse to run (no silent CPU path behind a device API)."""
     if _native.device_count() > 0:
         pytest.skip("a device is visible")
     L = _native.lib()
@@ -54,10 +55,18 @@ def test_no_device_per_call_takes_cpu_route_batches_fail_loudly():
     offs = np.zeros(1, dtype=np.uint64)
     lens = np.full(1, 9, dtype=np.uint32)
     res = np.zeros(1, dtype=np.uint32)
+    assert L.bkd_get_host_batch_route() == 1  # no device: the CPU route
     rc = L.bkd_crc_batch_host(0, b"123456789", 9, offs.ctypes.data, lens.ctypes.data, 1, None, 0, res.ctypes.data)
-    assert rc == -2  # BKD_ERR_NO_DEVICE: batches are GPU work
-    with pytest.raises(_native.BkdError):
-        ck.crc_batch_host(0, b"123456789", offs, lens)
+    assert rc == 0 and res[0] == 0xE3069283
+    with ck.host_batch_route(ck.HOST_ROUTE_GPU):
+        rc = L.bkd_crc_batch_host(0, b"123456789", 9, offs.ctypes.data, lens.ctypes.data, 1, None, 0,
+                                  res.ctypes.data)
+        assert rc == -2  # BKD_ERR_NO_DEVICE: the GPU route was asked for
+        with pytest.raises(_native.BkdError):
+            ck.crc_batch_host(0, b"123456789", offs, lens)
+    # device-resident batches are GPU work only
+    rc = L.bkd_crc_batch_uniform(0, 1 << 20, 4096, 4096, 1, None, 0, 1 << 21, None)
+    assert rc == -2
 
 
 @pytest.mark.parametrize("algo", [0, 1])
