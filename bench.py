@@ -241,9 +241,46 @@ def bucket_rates(ck, torch, algo, base, offs, lens, stream, steps: int) -> dict:
     return res
 
 
+def _route_name(ck, route: int) -> str:
+    return {ck.HOST_ROUTE_CPU: "cpu", ck.HOST_ROUTE_GPU: "gpu"}[route]
+
+
+def _host_reference_verify(frame_ptrs: np.ndarray, frame_lens: np.ndarray, n: int, ledger: int, algo: int,
+                           budget_s: float = 3.0) -> tuple[dict, np.ndarray]:
+    """cpu_baseline of the host-resident verify line: the reference's own loop over the same host
+    frames (BatchedReadOp.java:164-190 -> DigestManager.verifyDigest, two digest updates per frame)
+    on every host core — CRC32C through circe crc32c() compiled from /root/reference (oracle/_ref),
+    CRC32 through zlib's crc32() (= java.util.zip.CRC32)."""
+    import ctypes
+    import oracle
+    cores, why = host_cores()
+    st = np.zeros(n, dtype=np.int32)
+    stp = st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+    lp = np.ascontiguousarray(frame_lens, dtype=np.uint32)
+    if algo == 0 and oracle.ref() is not None:
+        kind, label = "reference", "circe crc32c() compiled from /root/reference, two calls per frame"
+        fn = oracle.ref().ref_verify_frames_timed
+    else:
+        kind, label = "port", "zlib crc32() (java.util.zip.CRC32's arithmetic), oracle/cpu_baseline.c"
+        fn = oracle.lib().oracle_zlib_verify_frames_timed
+
+    def run(thr, reps):
+        return fn(frame_ptrs.ctypes.data, lp.ctypes.data_as(oracle._u32p), n, ledger, 0, thr, reps, stp)
+    t1 = run(1, 1)
+    reps = max(1, int(budget_s / max(1e-6, t1 / cores)))
+    t = run(cores, reps)
+    nbytes = int(lp.sum())
+    return ({"value": round(nbytes * reps / t / GIB, 3), "unit": "GiB/s", "cores": cores, "kind": kind,
+             "single_core_value": round(nbytes / t1 / GIB, 3), "cpu_model": _cpu_model(), "cores_from": why,
+             "sample": f"the same {n} host frames ({nbytes / GIB:.3f} GiB), {reps} passes over {cores} threads, "
+                       f"DigestManager.verifyDigest per frame; {label}"}, st)
+
+
 def host_bench(args, ck, torch, rank) -> None:
-    """Config 5 fallback (no JVM/BookKeeper here): host-resident 4 KiB entries through the C-ABI
-    host path (pinned double-buffered H2D -> kernel -> D2H). PCIe-inclusive; never the headline."""
+    """Config 5 fallback (no JVM/BookKeeper here): host-resident 4 KiB entries, one contiguous host
+    buffer, through bkd_crc_batch_host: the automatic route (`value`) and each route on its own —
+    GPU = pinned double-buffered H2D -> kernel -> D2H, CPU = the library's threaded fold. End to end
+    from host memory; never the headline."""
     n = args.entries or (1 << 20)
     entry_len = 4096
     t = torch.empty(n * entry_len, dtype=torch.uint8, pin_memory=not args.pageable)
@@ -254,19 +291,35 @@ def host_bench(args, ck, torch, rank) -> None:
     host = t.numpy()
     offs = np.arange(n, dtype=np.uint64) * entry_len
     lens = np.full(n, entry_len, dtype=np.uint32)
-    for _ in range(max(1, args.warmup)):
-        ck.crc_batch_host(0, host, offs, lens)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = ck.crc_batch_host(0, host, offs, lens)
-    el = time.perf_counter() - t0
-    res = {"metric": "GiB/s CRC32C, host-resident 4 KiB entries incl. PCIe H2D/D2H (end-to-end, not the headline)",
-           "value": round(n * entry_len * args.steps / el / GIB, 2), "unit": "GiB/s", "n_gpus": 1,
-           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
-           "higher_is_better": True, "dtype": "u8",
+
+    def timed():
+        for _ in range(max(1, args.warmup)):
+            ck.crc_batch_host(0, host, offs, lens)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            got = ck.crc_batch_host(0, host, offs, lens)
+        return (time.perf_counter() - t0) / args.steps, got
+    auto = _route_name(ck, ck.get_host_batch_route())
+    el, out = timed()
+    routes = {}
+    for route in (ck.HOST_ROUTE_CPU, ck.HOST_ROUTE_GPU):
+        with ck.host_batch_route(route):
+            tr, got = timed()
+        assert (got == out).all(), "routes disagree"
+        routes[_route_name(ck, route)] = {"GiB_s": round(n * entry_len / tr / GIB, 2), "ms": round(tr * 1e3, 3)}
+    res = {"metric": "GiB/s CRC32C, host-resident 4 KiB entries, end to end from host memory (not the headline)",
+           "value": round(n * entry_len / el / GIB, 2), "unit": "GiB/s", "n_gpus": 1,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el * 1e3, 3),
+           "higher_is_better": True, "dtype": "u8", "route": auto, "routes": routes,
+           "host_threads": ck.get_host_threads(),
            "config": {"workload": f"{n} x {entry_len} B host-resident entries, "
-                                  f"{'pageable' if args.pageable else 'pinned'} source, 64 MiB double-buffered segments"},
+                                  f"{'pageable' if args.pageable else 'pinned'} source; GPU route: 64 MiB "
+                                  f"double-buffered segments incl. PCIe H2D/D2H; CPU route: host threads"},
            "digest_of_digests": int(np.bitwise_xor.reduce(out))}
+    if rank == 0 and not args.no_cpu_baseline:
+        cb, want = cpu_baseline(host, entry_len, 0, budget_s=3.0)
+        res["cpu_baseline"] = cb
+        res["parity_check"] = {"entries": n, "match": bool((want == out).all())}
     if rank == 0:
         print(json.dumps(res), flush=True)
 
@@ -274,8 +327,10 @@ def host_bench(args, ck, torch, rank) -> None:
 def digest_host_bench(args, ck, torch, rank, algo) -> None:
     """Config 5's workload without a JVM: framed 4 KiB entries that live in HOST
     memory as separate buffers (BatchedReadOp's ByteBufList, PendingAddOp's payloads), verified and
-    packaged through bkd_digest_verify_batch_host / bkd_digest_package_batch_host: gather into
-    pinned staging, H2D, the device sequence, D2H of statuses/frames. PCIe-inclusive, end to end."""
+    packaged through bkd_digest_verify_batch_host / bkd_digest_package_batch_host: the automatic
+    route (`value`) and each route on its own (GPU: gather into pinned staging, H2D, the device
+    sequence, D2H of statuses/frames; CPU: the library's threaded DigestManager arithmetic), next to
+    the reference's own per-frame verify loop on the same host cores (cpu_baseline)."""
     import ctypes
     from bookkeeper_amd import digest as dg
     from bookkeeper_amd._native import check, lib
@@ -305,6 +360,7 @@ def digest_host_bench(args, ck, torch, rank, algo) -> None:
                                                   vp(digests.ctypes.data)))
     package()
     host.reshape(n, L)[:, :32 + mac] = hdrs  # frames = [header][digest][payload], each its own 4 KiB buffer
+    first_digests = digests.copy()
     frame_ptrs = (base + ids.astype(np.uint64) * L).astype(np.uint64)
     frame_lens = np.full(n, L, dtype=np.uint32)
     status = np.zeros(n, dtype=np.int32)
@@ -323,19 +379,38 @@ def digest_host_bench(args, ck, torch, rank, algo) -> None:
             fn()
         return (time.perf_counter() - t0) / args.steps
     steps = args.steps
+    auto = _route_name(ck, ck.get_host_batch_route())
     t_verify = timed(verify)
     ok = bool((status == 0).all()) and first_bad.value == n
     t_pack = timed(package)
-    res = {"metric": "GiB/s framed 4 KiB ledger entries in host memory, batched DigestManager verify incl. "
-                     "gather + PCIe H2D/D2H (end to end; config 5's workload, not the headline)",
+    ok = ok and bool((digests == first_digests).all())
+    routes = {}
+    for route in (ck.HOST_ROUTE_CPU, ck.HOST_ROUTE_GPU):
+        with ck.host_batch_route(route):
+            tv = timed(verify)
+            rok = bool((status == 0).all()) and first_bad.value == n
+            tp = timed(package)
+            rok = rok and bool((digests == first_digests).all())
+        ok = ok and rok
+        routes[_route_name(ck, route)] = {"verify_GiB_s": round(n * L / tv / GIB, 2), "verify_ms": round(tv * 1e3, 3),
+                                          "package_GiB_s_payload": round(n * plen / tp / GIB, 2),
+                                          "package_ms": round(tp * 1e3, 3), "all_verified": rok}
+    res = {"metric": "GiB/s framed 4 KiB ledger entries in host memory, batched DigestManager verify, end to end "
+                     "(config 5's workload, not the headline)",
            "value": round(n * L / t_verify / GIB, 2), "unit": "GiB/s", "n_gpus": 1, "steps": steps,
            "warmup": args.warmup, "ms_per_step": round(t_verify * 1e3, 3), "higher_is_better": True, "dtype": "u8",
            "data": "synthetic (splitmix64, seed 42), pageable host memory, one 4 KiB buffer per entry",
            "config": {"workload": f"{n} framed entries x {L} B ({args.algo}) as separate host buffers "
-                                  f"(ByteBufList), 64 MiB double-buffered segments"},
+                                  f"(ByteBufList); GPU route: 64 MiB double-buffered segments incl. PCIe"},
+           "route": auto, "routes": routes, "host_threads": ck.get_host_threads(),
            "all_verified": ok, "entries_per_s": round(n / t_verify, 0),
            "package": {"GiB_s_payload": round(n * plen / t_pack / GIB, 2), "ms": round(t_pack * 1e3, 3),
                        "entries_per_s": round(n / t_pack, 0)}}
+    if rank == 0 and not args.no_cpu_baseline:
+        cb, st = _host_reference_verify(frame_ptrs, frame_lens, n, dm.ledgerId, algo)
+        res["cpu_baseline"] = cb
+        res["parity_check"] = {"entries": n, "match": bool((st == status).all())}
+        res["vs_cpu_baseline"] = round(res["value"] / cb["value"], 3)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if not ok:
@@ -377,11 +452,14 @@ def digest_bench(args, ck, torch, rank, dev, stream, algo) -> None:
         torch.cuda.synchronize()
         return a.elapsed_time(b) / 1e3 / args.steps
 
-    t_verify = timed(lambda: dm.verify_batch(framed, f_off, f_len, 0, stream=stream))
+    t_verify = t_pack = float("nan")
+    if args.digest_op in ("both", "verify"):
+        t_verify = timed(lambda: dm.verify_batch(framed, f_off, f_len, 0, stream=stream))
     status, first_bad = dm.verify_batch(framed, f_off, f_len, 0, stream=stream)
     torch.cuda.synchronize()
     ok = bool((status == 0).all().item()) and int(first_bad.item()) == n
-    t_pack = timed(lambda: dm.package_batch(ids, lacs, len_field, framed, pay_off, pay_len, stream=stream))
+    if args.digest_op in ("both", "package"):
+        t_pack = timed(lambda: dm.package_batch(ids, lacs, len_field, framed, pay_off, pay_len, stream=stream))
     # algorithmic bytes: verify reads every framed byte + 12 B of index, writes a 4 B status;
     # package reads the payload + 24 B of ids/LAC/length + 12 B of index, writes header+digest + 4 B
     v_bytes = n * (L + 12 + 4)
@@ -400,6 +478,8 @@ def digest_bench(args, ck, torch, rank, dev, stream, algo) -> None:
                         "algorithmic_bytes_per_launch": v_bytes},
            "package": {"GiB_s_payload": round(n * plen / t_pack / GIB, 2), "ms": round(t_pack * 1e3, 4),
                        "achieved_GB_s": round(p_bytes / t_pack / 1e9, 1),
+                       "frac": round(p_bytes / t_pack / 1e9 / HBM_PEAK_GBS, 4),
+                       "traffic": _pmc_traffic("package4k" if algo == ck.CRC32C else "package4k_crc32"),
                        "algorithmic_bytes_per_launch": p_bytes}}
     if rank == 0:
         print(json.dumps(res), flush=True)
@@ -431,6 +511,8 @@ def main() -> None:
     ap.add_argument("--plan-mode", type=int, default=0, help="0 auto, 1 direct, 2 chunked plan")
     ap.add_argument("--no-buckets", action="store_true", help="zipf: skip the per-bucket timings")
     ap.add_argument("--pageable", action="store_true", help="host4k: pageable instead of pinned host buffer")
+    ap.add_argument("--digest-op", default="both", choices=["both", "verify", "package"],
+                    help="verify4k: time verify, package or both (profiling one route's kernels alone)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL) on a real node; gloo only to rehearse several ranks on one GPU")
     args = ap.parse_args()

@@ -285,6 +285,19 @@ def fill_splitmix64(buf, seed: int, first_word: int = 0, stream=None) -> None:
                                         _stream_ptr(stream, buf)))
 
 
+def stream_sync(stream) -> None:
+    """Waits for `stream` and raises BKD_ERR_BOUNDS if an indexed batch enqueued on it since its
+    previous sync had an entry outside its base buffer (bkd_stream_sync; the flag is per stream)."""
+    ptr = _stream_ptr(stream)
+    sdev = getattr(stream, "device", None)
+    if sdev is not None:
+        import torch
+        with torch.cuda.device(sdev):
+            check(lib().bkd_stream_sync(ptr))
+    else:
+        check(lib().bkd_stream_sync(ptr))
+
+
 def release_stream(stream) -> None:
     """Waits for `stream` and frees the library's scratch for it (bkd_stream_release): call before a
     stream that ran indexed batches is dropped. Raises BKD_ERR_BOUNDS as a sync would."""

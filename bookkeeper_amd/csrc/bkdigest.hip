@@ -1052,12 +1052,15 @@ std::atomic<int> g_host_route{0};
 
 // The automatic choice, from the measured crossover (profiles/r03_host_route.log): a
 // host-resident batch through the GPU is bound by PCIe (~51 GiB/s) and, for separate entry buffers,
-// by the host gather into pinned staging, which costs the cores as much as folding the bytes; the
-// CPU route scales with the cores. BKD_HOST_ROUTE_MIN_THREADS overrides the crossover.
+// by the host gather into pinned staging; the CPU route scales with the cores until host memory
+// bandwidth. EPYC 9575F, 1M framed 4 KiB entries: GPU route 46.6 GiB/s verify / 50.6 contiguous;
+// CPU route 19.0 / 36.9 / 68.3 / 130 / 228 GiB/s verify at 1 / 2 / 4 / 8 / 16 threads (contiguous
+// 30.9 / 61.6 / 106 / 172 / 244) -> the CPU route from 3 threads with the AVX-512 fold. Without it
+// (128-bit fold, unmeasured on the box) from 4. BKD_HOST_ROUTE_MIN_THREADS overrides.
 int cpu_route_min_threads() {
     static const int t = [] {
         if (const char* v = getenv("BKD_HOST_ROUTE_MIN_THREADS")) return std::max(1, atoi(v));
-        return bkd::host::has_wide_fold() ? 2 : 4;
+        return bkd::host::has_wide_fold() ? 3 : 4;
     }();
     return t;
 }

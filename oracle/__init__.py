@@ -95,6 +95,10 @@ def lib():
                                                       _u32p]
         L.oracle_table.restype = None
         L.oracle_table.argtypes = [ctypes.c_int, _u32p]
+        L.oracle_zlib_verify_frames_timed.restype = ctypes.c_double
+        L.oracle_zlib_verify_frames_timed.argtypes = [ctypes.c_void_p, _u32p, ctypes.c_uint64, ctypes.c_int64,
+                                                      ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                                      ctypes.POINTER(ctypes.c_int32)]
         _lib = L
     return _lib
 

@@ -154,3 +154,72 @@ double oracle_pclmul_crc32_batch_timed(const uint8_t* base, const uint64_t* offs
     clock_gettime(CLOCK_MONOTONIC, &t1);
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
+
+/*
+ * BatchedReadOp's verify loop for a CRC-32 ledger (BatchedReadOp.java:164-190 ->
+ * DigestManager.verifyDigest, DigestManager.java:226-283, CRC32DigestManager.java:28-87): per frame
+ * zlib crc32() over the 32-byte header, resumed over the payload after the 8-byte digest, compared
+ * with the BE long at 32; then the ledger / entry ids. The CRC-32 counterpart of
+ * oracle/ref_shim.cpp's ref_verify_frames_timed (same status codes).
+ */
+typedef struct {
+    const uint8_t* const* frames;
+    const uint32_t* lens;
+    uint64_t lo, hi;
+    int64_t ledger, first;
+    int32_t* status;
+} zvjob;
+
+static uint64_t be_n(const uint8_t* p, int k) {
+    uint64_t v = 0;
+    for (int b = 0; b < k; ++b) v = (v << 8) | p[b];
+    return v;
+}
+
+static void* zvrun(void* p) {
+    zvjob* j = (zvjob*)p;
+    for (uint64_t i = j->lo; i < j->hi; ++i) {
+        const uint8_t* f = j->frames[i];
+        const uint32_t l = j->lens[i];
+        if (l < 40u) {
+            j->status[i] = 1;
+            continue;
+        }
+        uLong d = crc32(0L, f, 32);
+        d = crc32(d, f + 40, (uInt)(l - 40u));
+        if ((uint64_t)d != be_n(f + 32, 8)) j->status[i] = 2;
+        else if ((int64_t)be_n(f, 8) != j->ledger) j->status[i] = 3;
+        else if ((int64_t)be_n(f + 8, 8) != j->first + (int64_t)i) j->status[i] = 4;
+        else j->status[i] = 0;
+    }
+    return NULL;
+}
+
+double oracle_zlib_verify_frames_timed(const uint8_t* const* frames, const uint32_t* lens, uint64_t n, int64_t ledger,
+                                       int64_t first, int threads, int reps, int32_t* status) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    uint64_t cut[257];
+    uint64_t total = 0, acc = 0;
+    for (uint64_t i = 0; i < n; ++i) total += lens[i];
+    cut[0] = 0;
+    for (int t = 1; t <= threads; ++t) cut[t] = n;
+    int t = 1;
+    for (uint64_t i = 0; i < n && t < threads; ++i) {
+        acc += lens[i];
+        while (t < threads && acc * (uint64_t)threads >= total * (uint64_t)t) cut[t++] = i + 1;
+    }
+    pthread_t th[256];
+    zvjob jobs[256];
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int r = 0; r < reps; ++r) {
+        for (int k = 0; k < threads; ++k) {
+            jobs[k] = (zvjob){frames, lens, cut[k], cut[k + 1], ledger, first, status};
+            pthread_create(&th[k], NULL, zvrun, &jobs[k]);
+        }
+        for (int k = 0; k < threads; ++k) pthread_join(th[k], NULL);
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

@@ -693,6 +693,59 @@ def test_concurrent_callers(gpu):
     assert not errors, errors
 
 
+def test_eight_threads_eight_streams_no_global_lock(gpu):
+    """VERDICT r02 item 6 (SURVEY §8b "no global lock on the hot path"): 8 host threads, each with
+    its own stream, enqueue device batches back to back — plan, direct and uniform kinds, several
+    calls in flight per stream before one sync — while the per-stream scratch maps are read under a
+    shared lock only. Every digest is exact; each stream's bounds flag stays its own."""
+    import threading
+    import torch
+    rng = np.random.default_rng(88)
+    size = 6_000_000
+    data = oracle.fill_splitmix64(size, 5)
+    base = _dev_bytes(torch, data, gpu)
+    n = 4000
+    lens = rng.integers(0, 30000, n)
+    offs = np.array([rng.integers(0, size - l + 1) for l in lens], dtype=np.int64)
+    small_n = 60  # a 256 KiB window: the direct kernel
+    s_lens = rng.integers(0, 4000, small_n)
+    s_offs = rng.integers(0, (256 << 10) - 4000, small_n).astype(np.int64)
+    d_off, d_len = torch.from_numpy(offs).to(gpu), torch.from_numpy(lens.astype(np.int32)).to(gpu)
+    ds_off, ds_len = torch.from_numpy(s_offs).to(gpu), torch.from_numpy(s_lens.astype(np.int32)).to(gpu)
+    small_base = base[: 256 << 10]
+    want_p = oracle.batch(ck.CRC32C, data, offs, lens, seeds=np.full(n, 0, np.uint32))
+    want_s = oracle.batch(ck.CRC32, data[: 256 << 10], s_offs, s_lens, seeds=np.full(small_n, 0, np.uint32))
+    want_u = oracle.uniform(ck.CRC32C, data, 4096, 4096, size // 4096)
+    torch.cuda.synchronize()
+    errors = []
+    barrier = threading.Barrier(8)
+
+    def worker(k):
+        try:
+            st = torch.cuda.Stream(device=gpu)
+            outs = []
+            barrier.wait()
+            with torch.cuda.stream(st):
+                for r in range(12):
+                    outs.append(("plan", ck.crc_batch(ck.CRC32C, base, d_off, d_len, stream=st)))
+                    outs.append(("direct", ck.crc_batch(ck.CRC32, small_base, ds_off, ds_len, stream=st)))
+                    outs.append(("uniform", ck.crc_batch_uniform(ck.CRC32C, base, 4096, size // 4096, stream=st)))
+            ck.stream_sync(st)
+            for kind, got in outs:
+                w = {"plan": want_p, "direct": want_s, "uniform": want_u}[kind]
+                assert (got.cpu().numpy().view(np.uint32) == w).all(), (kind, k)
+            ck.release_stream(st)
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+
+    threads = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=240)
+    assert not errors, errors
+
+
 @pytest.mark.parametrize("size", [16383, 16384])
 @pytest.mark.parametrize("v2", [False, True])
 def test_composite_payload_digest_equals_contiguous(gpu, size, v2):

@@ -7,7 +7,10 @@ coalesced streaming read, so read bytes = 2 * FETCH_SIZE * 1024 for the streamin
 index/descriptor kernels (plan_*) are reported separately, raw (no correction: their accesses are
 not wide streaming reads).
 
-usage: pmc_summary.py FETCH_DIR WRITE_DIR CONFIG ALGO_BYTES_PER_LAUNCH [MAIN_KERNEL]"""
+usage: pmc_summary.py FETCH_DIR WRITE_DIR CONFIG ALGO_BYTES_PER_LAUNCH [MAIN_KERNEL [OTHER_KERNELS]]
+OTHER_KERNELS: comma-separated short names of the other kernels of the measured call (default: every
+other bkd:: kernel in the trace), e.g. the verify pipeline's gate/header/plan/finish launches when the
+same process also ran package calls."""
 import csv, glob, json, os, sys
 from collections import defaultdict
 
@@ -36,7 +39,7 @@ def median(v):
     return v[len(v) // 2] if v else 0.0
 
 
-def main(fetch_dir, write_dir, config, algo_bytes, main_kernel="bkd::crc_groups_kernel"):
+def main(fetch_dir, write_dir, config, algo_bytes, main_kernel="bkd::crc_groups_kernel", others=None):
     f = load(os.path.join(fetch_dir, "**", "*counter_collection.csv"))
     w = load(os.path.join(write_dir, "**", "*counter_collection.csv"))
     fetch_kb = median(f[main_kernel]["FETCH_SIZE"])
@@ -44,8 +47,9 @@ def main(fetch_dir, write_dir, config, algo_bytes, main_kernel="bkd::crc_groups_
     read_b = 2 * fetch_kb * 1024
     write_b = write_kb * 1024
     aux = {}
+    keep = set(others.split(",")) if others else None
     for k in sorted(set(f) | set(w)):
-        if k == main_kernel:
+        if k == main_kernel or (keep is not None and k not in keep):
             continue
         aux[k] = {"FETCH_SIZE_kB_median_raw": median(f[k]["FETCH_SIZE"]),
                   "WRITE_SIZE_kB_median": median(w[k]["WRITE_SIZE"])}
