@@ -21,6 +21,7 @@
  */
 #include <jni.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "bkdigest.h"
 
@@ -43,7 +44,20 @@ JNIEXPORT jint JNICALL Java_com_scurrilous_circe_crc_Sse42Crc32C_nativeArray(JNI
                                                                              jint length, jlong config) {
     (void)cls;
     (void)config;
-    /* pinned for the duration of the call only, as crc32c_sse42_jni.cpp:29-31 */
+    if (length <= 0) return current;
+    if ((uint64_t)length > bkd_get_cpu_route_max() && bkd_device_count() > 0) {
+        /* the GPU route (a PCIe round trip): copy the region out instead of holding the array's
+         * critical section, which stalls the JVM's collector, across it (the reference held it only
+         * for a CPU scan, crc32c_sse42_jni.cpp:29-31) */
+        jbyte* copy = (jbyte*)malloc((size_t)length);
+        if (!copy) return 0;
+        (*env)->GetByteArrayRegion(env, input, index, length, copy);
+        jint crc = 0;
+        if (!(*env)->ExceptionCheck(env)) crc = resume_host_or_zero(current, copy, length);
+        free(copy);
+        return crc;
+    }
+    /* the CPU route: pinned for the duration of the scan only, as crc32c_sse42_jni.cpp:29-31 */
     jbyte* buf = (jbyte*)(*env)->GetPrimitiveArrayCritical(env, input, 0);
     if (!buf) return 0;
     const jint crc = resume_host_or_zero(current, buf + index, length);

@@ -429,6 +429,55 @@ def test_verify_batch_near_uniform_frames(gpu, dtype, algo, skip):
         assert int(first_bad.item()) == (int(nz[0]) if nz.size else n)
 
 
+@pytest.mark.parametrize("lanes,n,plen_mid", [(4, 70000, 300), (16, 20000, 4000), (32, 10000, 4000),
+                                               (64, 5000, 4000)])
+def test_verify_fused_route_every_lane_width(gpu, lanes, n, plen_mid):
+    """crc_verify_fused_kernel is instantiated for G = 4/8/16/32/64; each width is reached
+    with the plan geometry at that lane count and frames sized so that the automatic lane choice for
+    one frame per group equals it (the fused route's condition). Statuses and the verified prefix
+    equal oracle.verify_entry's, with payload, digest and id corruptions."""
+    import torch
+    rng = np.random.default_rng(lanes)
+    ledger, first = 44, 100
+    algo = ck.CRC32C
+    dm = dg.DigestManager.instantiate(ledger, b"", dg.DigestType.CRC32C, False)
+    plen = rng.integers(plen_mid - plen_mid // 40, plen_mid + plen_mid // 40, n)
+    payload = oracle.fill_splitmix64(int(plen.sum()), 29)
+    poffs = np.concatenate([[0], np.cumsum(plen[:-1])])
+    frames = []
+    for i in range(n):
+        p = payload[poffs[i]:poffs[i] + plen[i]]
+        d, hdr = oracle.digest_entry(algo, ledger, first + i, first + i - 1, int(plen[i]), p)
+        frames.append(bytearray(hdr + oracle.digest_bytes(algo, d) + p.tobytes()))
+    for k, (pos, bit) in enumerate(((50, 0x01), (34, 0x80), (7, 0x02), (15, 0x04))):
+        frames[(k + 1) * n // 5][pos] ^= bit  # payload, digest, ledger id, entry id
+    gaps = rng.integers(0, 9, n)
+    flens = np.array([len(f) for f in frames], dtype=np.int64)
+    foffs = np.concatenate([[0], np.cumsum(flens[:-1] + gaps[:-1])]) + 3
+    blob = np.zeros(int(foffs[-1] + flens[-1]) + 64, dtype=np.uint8)
+    for i in range(n):
+        blob[foffs[i]:foffs[i] + flens[i]] = np.frombuffer(bytes(frames[i]), dtype=np.uint8)
+    # the library's automatic lane choice for one frame per group (bkdigest.hip auto_lanes)
+    cus = torch.cuda.get_device_properties(gpu).multi_processor_count
+    mean = blob.size // n
+    g = 4 if mean < 512 else (8 if mean < 32768 else 32)
+    while g < 64 and n * g < cus * 1024:
+        g *= 2
+    assert g == lanes, (g, lanes)
+    want = np.array([oracle.verify_entry(algo, bytes(frames[i]), ledger, first + i) for i in range(n)])
+    steps = min(32, 32768 // (16 * lanes))
+    ck.set_plan_geometry(lanes, steps, 16)
+    try:
+        status, first_bad = dm.verify_batch(_dev_bytes(torch, blob, gpu), torch.from_numpy(foffs).to(gpu),
+                                            torch.from_numpy(flens.astype(np.int32)).to(gpu), first_entry_id=first)
+        status = status.cpu().numpy()
+    finally:
+        ck.set_plan_geometry()
+    bad = np.nonzero(status != want)[0]
+    assert bad.size == 0, (bad[:5], status[bad[:5]], want[bad[:5]])
+    assert int(first_bad.item()) == int(np.nonzero(want)[0][0])
+
+
 def test_plan_overflow_falls_back_to_direct(gpu):
     """Heavily overlapping entries exceed the plan's capacity (n + size/CH + 16 chunks); the
     overflowing entries are computed one entry per group in the chunk kernel's tail, bit-exact."""
