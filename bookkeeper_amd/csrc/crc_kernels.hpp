@@ -60,6 +60,10 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
+#ifndef BKD_MAIN_XOR3
+#define BKD_MAIN_XOR3 0  // build-time variant: the main fold's five-way XOR as two v_bitop3 (tools/ab_libs.py)
+#endif
+
 // v * C_main via the replicated tables. lanereg = 4*(lane&31) | 1<<16.
 // v_perm_b32 result bytes (b3..b0) = (0, hi, v.byte_t, 4*(lane&31)); hi = 1 selects the
 // upper 64 KiB half (tables 2, 3); the +128 immediate selects the odd table of a pair.
@@ -69,8 +73,12 @@ __device__ __forceinline__ uint32_t mul_main_add(const uint32_t* lds, uint32_t v
     const uint32_t a1 = __builtin_amdgcn_perm(v, lanereg, 0x0C0C0500u);
     const uint32_t a2 = __builtin_amdgcn_perm(v, lanereg, 0x0C020600u);
     const uint32_t a3 = __builtin_amdgcn_perm(v, lanereg, 0x0C020700u);
+#if BKD_MAIN_XOR3
+    return xor3(xor3(lds_word(lds, a0), lds_word(lds, a1 + 128u), lds_word(lds, a2)), lds_word(lds, a3 + 128u), d);
+#else
     // plain XORs: consumed in issue order (a v_bitop3 here measured up to 10 % slower on short entries)
     return lds_word(lds, a0) ^ lds_word(lds, a1 + 128u) ^ lds_word(lds, a2) ^ lds_word(lds, a3 + 128u) ^ d;
+#endif
 }
 
 __device__ __forceinline__ uint32_t mul_main(const uint32_t* lds, uint32_t v, uint32_t lanereg) {

@@ -43,7 +43,7 @@ def main() -> None:
         d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
         out = torch.empty(n, dtype=torch.int32, device=dev)
         res = {}
-        for mode in (2, 1):
+        for mode in [int(m) for m in os.environ.get("HEADS_MODES", "2 1").split()]:
             ck.set_plan_mode(mode)
             for _ in range(3):
                 ck.crc_batch(ck.CRC32C, base, d_off, d_len, out=out, stream=st)
@@ -58,7 +58,8 @@ def main() -> None:
             print(json.dumps({"J": J, "mode": "plan" if mode == 2 else "direct", "n": n, "mean_len": float(lens[:-1].mean()),
                               "ms": round(t * 1e3, 4), "GB_s": round(total / t / 1e9, 1),
                               "us_per_round": round(t * 1e6 / (n / groups), 3)}), flush=True)
-        assert torch.equal(res[1], res[2]), J
+        if 1 in res and 2 in res:
+            assert torch.equal(res[1], res[2]), J
         del base, d_off, d_len, out
         torch.cuda.empty_cache()
     ck.set_plan_mode(0)

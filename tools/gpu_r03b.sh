@@ -22,4 +22,19 @@ for op in verify package; do
   echo "== pmc fetch $op"; timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_$op -o pmc -- python3 $R/bench.py --config verify4k --digest-op $op --steps 5 --warmup 1 > $O/pmc_fetch_$op.log 2>&1 || { tail -5 $O/pmc_fetch_$op.log; exit 1; }
   echo "== pmc write $op"; timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write_$op -o pmc -- python3 $R/bench.py --config verify4k --digest-op $op --steps 5 --warmup 1 > $O/pmc_write_$op.log 2>&1 || { tail -5 $O/pmc_write_$op.log; exit 1; }
 done
+cd $R
+echo "== ramp A/B (xor3 main fold vs plain)"
+for lib in bookkeeper_amd/libbkdigest.so tools/variants/lib_xor3.so bookkeeper_amd/libbkdigest.so tools/variants/lib_xor3.so; do
+  timeout -k 10 120 python3 tools/ramp.py --lib $lib --rounds 2 --idle-ms 1500 --launches 100 >> $O/ramp_ab.log 2>&1 || { tail -5 $O/ramp_ab.log; exit 1; }
+done
+python3 - <<'PY'
+import json, os
+O = os.environ.get("GRAFT_REPO_ROOT", "/root/repo") + "/gpurun_out/r03b"
+for line in open(os.path.join(O, "ramp_ab.log")):
+    if line.startswith("{"):
+        d = json.loads(line)
+        print(d["lib"], d["round"], d["mean_0_5"], d["mean_5_25_driver_window"], d["mean_25_50"], d["mean_50_150_builder_window"])
+PY
+echo "== ab_libs"; AB_ROUNDS=3 timeout -k 10 600 python3 tools/ab_libs.py > $O/ab_libs.log 2>&1 || { tail -5 $O/ab_libs.log; exit 1; }
+tail -30 $O/ab_libs.log
 echo done

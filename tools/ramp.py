@@ -24,9 +24,19 @@ def main() -> None:
     ap.add_argument("--idle-ms", type=float, default=0.0, help="host sleep before the first launch")
     ap.add_argument("--touch", action="store_true", help="read the whole buffer once (torch sum) before launching")
     ap.add_argument("--rounds", type=int, default=1, help="bursts, each after --idle-ms of host sleep")
+    ap.add_argument("--lib", default=None, help="a libbkdigest.so build to time (default: the package's)")
     args = ap.parse_args()
     import torch
     from bookkeeper_amd import checksum as ck
+    if args.lib:  # a variant build: the checksum wrappers call it through _native.lib()
+        import ctypes
+        from bookkeeper_amd import _native
+        L = ctypes.CDLL(os.path.abspath(args.lib))
+        for fn, (res, argt) in _native.PROTOTYPES.items():
+            if hasattr(L, fn):
+                getattr(L, fn).restype = res
+                getattr(L, fn).argtypes = argt
+        _native._lib = L
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     n, L = 1 << 20, 4096
@@ -58,7 +68,7 @@ def burst(args, torch, ck, base, out, stream, L, n, rnd):
     def mean(lo, hi):
         w = ms[lo:hi]
         return round(sum(w) / len(w), 4) if w else None
-    res = {"round": rnd, "launches": args.launches, "idle_ms": args.idle_ms, "touch": args.touch,
+    res = {"lib": args.lib or "bookkeeper_amd/libbkdigest.so", "round": rnd, "launches": args.launches, "idle_ms": args.idle_ms, "touch": args.touch,
            "first10_ms": [round(x, 4) for x in ms[:10]],
            "mean_0_5": mean(0, 5), "mean_5_25_driver_window": mean(5, 25), "mean_25_50": mean(25, 50),
            "mean_50_150_builder_window": mean(50, 150), "mean_150_end": mean(150, args.launches),
