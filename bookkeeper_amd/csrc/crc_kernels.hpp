@@ -60,6 +60,10 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
+#ifndef BKD_EARLY_PREFETCH
+#define BKD_EARLY_PREFETCH 1
+#endif
+
 #ifndef BKD_MAIN_XOR3
 #define BKD_MAIN_XOR3 0  // build-time variant: the main fold's five-way XOR as two v_bitop3 (tools/ab_libs.py)
 #endif
@@ -801,6 +805,14 @@ __device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lan
     using Gm = Geo<G>;
     const int64_t a = c.a;
     const int32_t d0 = c.d0;
+    const uint32_t rem = c.J - 1u;
+#if BKD_EARLY_PREFETCH
+    // the successor is requested before anything waits for this chunk's own blocks (unconditionally,
+    // so that the loads land in NW0/NA without a register copy): the compiler's s_waitcnt for W0 then
+    // sits after these loads, and consecutive chunks overlap their memory round trips instead of
+    // paying one each
+    chunk_prefetch<G, PF, NT>(base, nx, NW0, NA);
+#endif
     u32x4 w;
     if (d0 <= 0) w = W0;
     else if (d0 < 16) w = mask_low_bytes(W0, (uint32_t)d0);
@@ -821,7 +833,6 @@ __device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lan
     uint32_t fx = 0u;
     if (d0 > Gm::kStep - 4) fx = place_seed(r0, d0 - Gm::kStep);
     uint32_t c0 = w.x, c1 = w.y, c2 = w.z, c3 = w.w;
-    const uint32_t rem = c.J - 1u;
     // long chunk with a pad in this lane's last block: that block again, requested now (its line is
     // in cache by the time it is used), instead of selecting it among the A/B sets afterwards
     // (Zipf -0.5 % in both A/B orders)
@@ -843,7 +854,9 @@ __device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lan
         c3 = mul_main_add(lds, c3, lanereg, (d).w);     \
     } while (0)
     if (rem <= (uint32_t)PF) {
+#if !BKD_EARLY_PREFETCH
         chunk_prefetch<G, PF, NT>(base, nx, NW0, NA);
+#endif
         if (rem > 0u) BKD_FOLD0(A[0]);
 #pragma unroll
         for (int k = 1; k < PF; ++k)
@@ -877,7 +890,9 @@ __device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lan
 #pragma unroll
         for (int k = 0; k < PF; ++k)
             if ((uint32_t)(PF + k) < left) A[k] = ld16<NT>(p + (int64_t)(PF + k) * Gm::kStep);
+#if !BKD_EARLY_PREFETCH
         chunk_prefetch<G, PF, NT>(base, nx, NW0, NA);  // issued after every load of this chunk
+#endif
 #pragma unroll
         for (int k = 0; k < PF; ++k)
             if ((uint32_t)k < left) BKD_FOLD(B[k]);

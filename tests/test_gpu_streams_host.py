@@ -458,3 +458,25 @@ def test_plan_short_entries_among_long(gpu):
         assert (out.cpu().numpy().view(np.uint32) == want).all()
     finally:
         ck.set_plan_mode(0)
+
+
+def test_host_release_frees_idle_staging_and_restarts(gpu):
+    """the GPU route's pinned staging sets can be released (bkd_host_release) by a
+    long-lived process; the next host-resident batch through the GPU creates them again and stays
+    exact, for verify (first_bad word only) and package (aux + frame buffers)."""
+    algo = ck.CRC32C
+    ledger, first = 3, 10
+    dm = dg.DigestManager.instantiate(ledger, b"", dg.DigestType.CRC32C)
+    rng = np.random.default_rng(123)
+    frames = _frames(algo, rng, 500, ledger, first, 5000)
+    want = np.array([oracle.verify_entry(algo, bytes(f), ledger, first + i) for i, f in enumerate(frames)])
+    with ck.host_batch_route(ck.HOST_ROUTE_GPU):
+        for _ in range(2):
+            st, fb = dm.verify_batch_host(frames, first)
+            assert (st == want).all() and fb == len(frames)
+            payloads = [bytes(f[36:]) for f in frames]
+            ids = np.arange(len(frames), dtype=np.int64) + first
+            hdrs, digests = dm.package_batch_host(ids, ids - 1, np.array([len(p) for p in payloads]), payloads)
+            for i in range(0, len(frames), 37):
+                assert bytes(hdrs[i]) == bytes(frames[i][:36])
+            ck.host_release()

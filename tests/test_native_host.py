@@ -225,3 +225,15 @@ def test_host_batch_wrapper_validates_index_sizes():
         ck.crc_batch_host(ck.CRC32C, data, [0, 10, 20], [5, 5])
     with pytest.raises(ValueError):
         ck.crc_batch_host(ck.CRC32C, data, [0, 10], [5, 5], seeds=[1])
+
+
+def test_host_release_and_route_knobs_without_device():
+    """bkd_host_release with nothing staged, route and thread knobs: validation and round trips."""
+    L = _native.lib()
+    assert L.bkd_host_release() == 0
+    assert L.bkd_set_host_batch_route(3) == -1 and L.bkd_set_host_batch_route(-1) == -1
+    assert L.bkd_set_host_threads(-2) == -1
+    assert L.bkd_set_host_threads(1) == 0 and L.bkd_get_host_threads() == 1
+    assert L.bkd_set_host_threads(0) == 0 and L.bkd_get_host_threads() >= 1
+    with ck.host_batch_route(ck.HOST_ROUTE_CPU):
+        assert ck.get_host_batch_route() == ck.HOST_ROUTE_CPU
