@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <type_traits>
 
 namespace bkd {
@@ -61,7 +62,13 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 }
 
 #ifndef BKD_EARLY_PREFETCH
-#define BKD_EARLY_PREFETCH 1
+#define BKD_EARLY_PREFETCH 0
+#endif
+#ifndef BKD_TAIL_UNCOND
+#define BKD_TAIL_UNCOND 0  // build-time variant: unconditional tail loads in the A/B fold loops
+#endif
+#ifndef BKD_CHUNK_UNROLL
+#define BKD_CHUNK_UNROLL 2  // chunk halves per iteration of the chunk kernel's loop (2, 4 or 8)
 #endif
 
 #ifndef BKD_MAIN_XOR3
@@ -335,7 +342,10 @@ __device__ __forceinline__ void stage_tables(uint32_t* lds, const uint32_t* __re
 // ALIGNED: `e` is 16-byte aligned in device memory, so every lane address is aligned; the lane
 // straddling s loads its aligned block and clears the bytes before s (any e - s >= 1 works).
 // Otherwise the straddling lane loads 16 bytes at s (needs e - s >= 16) and shifts them up.
-template <int G, int PF, bool NT, bool ALIGNED>
+// TAILU: unconditional tail loads (see below); taken for uniform batches, where it measured −0.6 %
+// (1M x 4 KiB, same-process A/B in both library orders) while indexed and framed batches did not
+// gain (package +1.5 %), profiles/r03f_ab_variants_order*.log
+template <int G, int PF, bool NT, bool ALIGNED, bool TAILU = BKD_TAIL_UNCOND != 0>
 __device__ __forceinline__ uint32_t fold_range(const uint32_t* lds, uint32_t lanereg, int g,
                                                const uint8_t* __restrict__ base, int64_t s, int64_t e, uint32_t r0) {
     using Gm = Geo<G>;
@@ -405,15 +415,31 @@ __device__ __forceinline__ uint32_t fold_range(const uint32_t* lds, uint32_t lan
             left -= 2u * PF;
         }
         // Tail: A holds PF loaded steps; `left` (< 2PF) steps remain unloaded.
+        if constexpr (TAILU) {
+            // every tail load is issued (a step past the range reloads the range's last loaded step):
+            // the load count does not depend on `left`
 #pragma unroll
-        for (int k = 0; k < PF; ++k)
-            if ((uint32_t)k < left) B[k] = ld16<NT>(p + (int64_t)k * Gm::kStep);
+            for (int k = 0; k < PF; ++k)
+                B[k] = ld16<NT>(p + (int64_t)std::min<int32_t>(k, (int32_t)left - 1) * Gm::kStep);
+            asm volatile("" ::: "memory");  // keeps the loads here: not sunk into the conditional folds
+        } else {
+#pragma unroll
+            for (int k = 0; k < PF; ++k)
+                if ((uint32_t)k < left) B[k] = ld16<NT>(p + (int64_t)k * Gm::kStep);
+        }
         BKD_FOLD0(A[0]);
 #pragma unroll
         for (int k = 1; k < PF; ++k) BKD_FOLD(A[k]);
+        if constexpr (TAILU) {
 #pragma unroll
-        for (int k = 0; k < PF; ++k)
-            if ((uint32_t)(PF + k) < left) A[k] = ld16<NT>(p + (int64_t)(PF + k) * Gm::kStep);
+            for (int k = 0; k < PF; ++k)
+                A[k] = ld16<NT>(p + (int64_t)std::min<int32_t>(PF + k, (int32_t)left - 1) * Gm::kStep);
+            asm volatile("" ::: "memory");
+        } else {
+#pragma unroll
+            for (int k = 0; k < PF; ++k)
+                if ((uint32_t)(PF + k) < left) A[k] = ld16<NT>(p + (int64_t)(PF + k) * Gm::kStep);
+        }
 #pragma unroll
         for (int k = 0; k < PF; ++k)
             if ((uint32_t)k < left) BKD_FOLD(B[k]);
@@ -459,7 +485,8 @@ __device__ __forceinline__ void groups_loop(const uint32_t* lds, uint32_t lanere
             continue;
         }
         const uint32_t v =
-            fold_range<G, PF, NT, false>(lds, lanereg, g, base, wk.s, wk.s + (int64_t)wk.len, wk.r0);
+            fold_range<G, PF, NT, false, BKD_TAIL_UNCOND != 0 || std::is_same<Src, UniformSrc>::value>(
+                lds, lanereg, g, base, wk.s, wk.s + (int64_t)wk.len, wk.r0);
         if (g == 0) *wk.dst = v ^ wk.xorout;
     }
 }
@@ -837,7 +864,13 @@ __device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lan
     // in cache by the time it is used), instead of selecting it among the A/B sets afterwards
     // (Zipf -0.5 % in both A/B orders)
     u32x4 relast = u32x4{0u, 0u, 0u, 0u};
+#if BKD_TAIL_UNCOND
+    // requested by every long chunk (the lane's last block, always inside the window), so that the
+    // number of loads in flight does not depend on the pad and the waits stay exact
+    if (rem > (uint32_t)PF) relast = ld16<false>(base + a + (int64_t)rem * Gm::kStep);
+#else
     if (rem > (uint32_t)PF && c.pad && c.keep < 16) relast = ld16<false>(base + a + (int64_t)rem * Gm::kStep);
+#endif
 #define BKD_FOLD0(d)                                     \
     do {                                                 \
         c0 = mul_main_add(lds, c0, lanereg, (d).x ^ fx);    \
@@ -880,16 +913,29 @@ __device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lan
             p += (int64_t)(2 * PF) * Gm::kStep;
             left -= 2u * PF;
         }
+#if BKD_TAIL_UNCOND
+#pragma unroll
+        for (int k = 0; k < PF; ++k) B[k] = ld16<NT>(p + (int64_t)std::min<int32_t>(k, (int32_t)left - 1) * Gm::kStep);
+        asm volatile("" ::: "memory");  // keeps the loads here: not sunk into the conditional folds
+#else
 #pragma unroll
         for (int k = 0; k < PF; ++k)
             if ((uint32_t)k < left) B[k] = ld16<NT>(p + (int64_t)k * Gm::kStep);
+#endif
         if (first) BKD_FOLD0(A[0]);
         else BKD_FOLD(A[0]);
 #pragma unroll
         for (int k = 1; k < PF; ++k) BKD_FOLD(A[k]);
+#if BKD_TAIL_UNCOND
+#pragma unroll
+        for (int k = 0; k < PF; ++k)
+            A[k] = ld16<NT>(p + (int64_t)std::min<int32_t>(PF + k, (int32_t)left - 1) * Gm::kStep);
+        asm volatile("" ::: "memory");
+#else
 #pragma unroll
         for (int k = 0; k < PF; ++k)
             if ((uint32_t)(PF + k) < left) A[k] = ld16<NT>(p + (int64_t)(PF + k) * Gm::kStep);
+#endif
 #if !BKD_EARLY_PREFETCH
         chunk_prefetch<G, PF, NT>(base, nx, NW0, NA);  // issued after every load of this chunk
 #endif
@@ -974,6 +1020,19 @@ __device__ __forceinline__ void plan_chunks_loop(const uint32_t* lds, uint32_t l
     for (;;) {
         BKD_CHUNK_HALF(dA, W0x, Ax, Bx, W0y, Ay)  // chunk i in set X, prefetch into Y
         BKD_CHUNK_HALF(dB, W0y, Ay, By, W0x, Ax)  // chunk i in set Y, prefetch into X
+#if BKD_CHUNK_UNROLL >= 4
+        // the back edge copies the loop-carried descriptor registers, for which the compiler waits
+        // with s_waitcnt vmcnt(0) — a full drain of the loads in flight; more halves per iteration,
+        // fewer drains
+        BKD_CHUNK_HALF(dA, W0x, Ax, Bx, W0y, Ay)
+        BKD_CHUNK_HALF(dB, W0y, Ay, By, W0x, Ax)
+#endif
+#if BKD_CHUNK_UNROLL >= 8
+        BKD_CHUNK_HALF(dA, W0x, Ax, Bx, W0y, Ay)
+        BKD_CHUNK_HALF(dB, W0y, Ay, By, W0x, Ax)
+        BKD_CHUNK_HALF(dA, W0x, Ax, Bx, W0y, Ay)
+        BKD_CHUNK_HALF(dB, W0y, Ay, By, W0x, Ax)
+#endif
     }
 #undef BKD_CHUNK_HALF
 }
