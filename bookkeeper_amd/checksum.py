@@ -402,7 +402,8 @@ def set_plan_geometry(lanes: int = 8, steps_per_chunk: int = 32, merge_bytes: in
 
 
 def host_tables(algo: int, lanes: int) -> np.ndarray:
-    n = (2 + int(np.log2(lanes))) * 1024 + 256 + 2048
+    # operator sets, byte table, x^64 / x^96 sets, and for 4 / 8 lanes the lane-position nibble tables
+    n = (2 + int(np.log2(lanes))) * 1024 + 256 + 2048 + (128 * lanes if lanes in (4, 8) else 0)
     out = np.zeros(n, dtype=np.uint32)
     check(lib().bkd_host_tables(algo, lanes, ctypes.c_void_p(out.ctypes.data), n))
     return out

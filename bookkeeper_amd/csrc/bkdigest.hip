@@ -1234,6 +1234,8 @@ int bkd_crc_batch_uniform(int algo, const void* d_base, uint64_t stride, uint32_
     int lanes = auto_lanes(entry_len, n, ds->cus);
     if (g_forced_lanes.load() == 0 && entry_len >= 16u && entry_len <= 48u && n >= (uint64_t)ds->cus * bkd::kBlock)
         lanes = 1;
+    if (lanes == 8 && entry_len >= bkd::kTailUncondSteps * 16u * 8u)  // measured at 8 lanes only
+        return dispatch_lanes(*ds, lanes, algo, (const uint8_t*)d_base, bkd::UniformLongSrc{src}, n, st);
     return dispatch_lanes(*ds, lanes, algo, (const uint8_t*)d_base, src, n, st);
 }
 

@@ -36,18 +36,25 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kBlock = 1024;          // 16 waves per CU, one workgroup per CU (LDS-limited)
 constexpr uint32_t kMainBytes = 131072u;  // 4 tables x 256 entries x 32 banks x 4 B
 
+#ifndef BKD_LANE_POS
+#define BKD_LANE_POS 1  // groups of 4 / 8 lanes finish by lane-position tables + DPP XOR (finish_lanes)
+#endif
+
 template <int G>
 struct Geo {
     static_assert(G == 1 || G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "group width");
     static constexpr int kLevels = G == 1 ? 0 : G == 4 ? 2 : G == 8 ? 3 : G == 16 ? 4 : G == 32 ? 5 : 6;
     // Groups of <= 16 lanes sit inside one DPP row and have LDS room for the x^64/x^96 sets.
     static constexpr bool kFast = G <= 16;
-    static constexpr int kCompactWords = (2 + kLevels) * 1024 + 256 + 2048;
+    // Groups of 4 / 8 lanes also stage the lane-position nibble tables (crc_tables.hpp).
+    static constexpr bool kLaneTab = BKD_LANE_POS && (G == 4 || G == 8);
+    static constexpr int kCompactWords = (2 + kLevels) * 1024 + 256 + 2048 + (kLaneTab ? 128 * G : 0);
     static constexpr int kAuxWords = kCompactWords - 1024 - (kFast ? 0 : 2048);  // staged after the main set
     static constexpr uint32_t kX32Off = kMainBytes;  // LDS byte offset of the x^32 set
     static constexpr uint32_t kByteTabOff = kMainBytes + (1 + kLevels) * 4096u;
     static constexpr uint32_t kX64Off = kByteTabOff + 1024u;
     static constexpr uint32_t kX96Off = kX64Off + 4096u;
+    static constexpr uint32_t kLaneOff = kX96Off + 4096u;
     static constexpr int kLdsWords = (int)(kMainBytes / 4) + kAuxWords;
     static constexpr int64_t kStep = 16 * G;
 };
@@ -170,6 +177,11 @@ struct UniformSrc {
         return 0;
     }
 };
+
+// Uniform entries of at least kTailUncondSteps steps in 8-lane groups: the same work items, folded
+// with unconditional tail loads (fold_range's TAILU; chosen on the host from the entry length).
+constexpr uint32_t kTailUncondSteps = 32;
+struct UniformLongSrc : UniformSrc {};
 
 struct IndexedSrc {
     uint64_t n;
@@ -294,6 +306,19 @@ __device__ __forceinline__ uint32_t finish_lanes(const uint32_t* lds, uint32_t c
         const uint32_t lanereg = ((uint32_t)(threadIdx.x & 31) << 2) | (1u << 16);
         return mul_main_add(lds, c0, lanereg,
                             mul_aux_add(lds, Gm::kX96Off, c1, mul_aux_add(lds, Gm::kX64Off, c2, mul_aux(lds, Gm::kX32Off, c3))));
+    } else if constexpr (Gm::kLaneTab) {
+        // one more product per lane, by its weight x^(128 (G-1-g)) in the group's register (eight
+        // nibble lookups, independent), then an XOR over the group's lanes by DPP: one dependent
+        // LDS round trip instead of log2(G)
+        const uint32_t v = xor3(mul_aux(lds, Gm::kX32Off + 4096u, c0), mul_aux(lds, Gm::kX96Off, c1),
+                                mul_aux_add(lds, Gm::kX64Off, c2, mul_aux(lds, Gm::kX32Off, c3)));
+        const uint32_t lb = Gm::kLaneOff + 4u * (uint32_t)(threadIdx.x & (G - 1));
+        auto nib = [&](int k) { return lds_word(lds, lb + 64u * G * (uint32_t)k + ((v >> (4 * k)) & 15u) * (4u * G)); };
+        uint32_t r = xor3(xor3(nib(0), nib(1), nib(2)), xor3(nib(3), nib(4), nib(5)), nib(6) ^ nib(7));
+        r ^= dpp_row_shl<1>(r);
+        r ^= dpp_row_shl<2>(r);
+        if constexpr (G == 8) r ^= dpp_row_shl<4>(r);
+        return r;
     } else if constexpr (Gm::kFast) {
         const uint32_t v = xor3(mul_aux(lds, Gm::kX32Off + 4096u, c0), mul_aux(lds, Gm::kX96Off, c1),
                                 mul_aux_add(lds, Gm::kX64Off, c2, mul_aux(lds, Gm::kX32Off, c3)));
@@ -342,9 +367,11 @@ __device__ __forceinline__ void stage_tables(uint32_t* lds, const uint32_t* __re
 // ALIGNED: `e` is 16-byte aligned in device memory, so every lane address is aligned; the lane
 // straddling s loads its aligned block and clears the bytes before s (any e - s >= 1 works).
 // Otherwise the straddling lane loads 16 bytes at s (needs e - s >= 16) and shifts them up.
-// TAILU: unconditional tail loads (see below); taken for uniform batches, where it measured −0.6 %
-// (1M x 4 KiB, same-process A/B in both library orders) while indexed and framed batches did not
-// gain (package +1.5 %), profiles/r03f_ab_variants_order*.log
+// TAILU: unconditional tail loads (see below); taken for uniform batches of >= kTailUncondSteps
+// steps, where it measured −0.6 % (1M x 4 KiB, same-process A/B in both library orders,
+// profiles/r03f_ab_variants_order*.log); indexed and framed batches did not gain (package +1.5 %),
+// and short uniform entries lost (512 B +13 %, 1 KiB +2.7 %: most of their loads are tail loads,
+// profiles/r03g_ab_order*.log)
 template <int G, int PF, bool NT, bool ALIGNED, bool TAILU = BKD_TAIL_UNCOND != 0>
 __device__ __forceinline__ uint32_t fold_range(const uint32_t* lds, uint32_t lanereg, int g,
                                                const uint8_t* __restrict__ base, int64_t s, int64_t e, uint32_t r0) {
@@ -485,7 +512,7 @@ __device__ __forceinline__ void groups_loop(const uint32_t* lds, uint32_t lanere
             continue;
         }
         const uint32_t v =
-            fold_range<G, PF, NT, false, BKD_TAIL_UNCOND != 0 || std::is_same<Src, UniformSrc>::value>(
+            fold_range<G, PF, NT, false, BKD_TAIL_UNCOND != 0 || std::is_same<Src, UniformLongSrc>::value>(
                 lds, lanereg, g, base, wk.s, wk.s + (int64_t)wk.len, wk.r0);
         if (g == 0) *wk.dst = v ^ wk.xorout;
     }

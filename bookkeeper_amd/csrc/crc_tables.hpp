@@ -75,8 +75,13 @@ inline int log2_lanes(int lanes) {
 //   set 2+s, s<log2 lanes: x^(128 * 2^s)            (lane-tree level s: a block of 2^s lanes = 16*2^s bytes)
 //   256 words            : byte table x^8           (serial paths; equals ReflectedIntCrc's table)
 //   2 more sets          : x^64, x^96               (one-level in-lane combine of the 4 dword streams)
+//   groups of 4 / 8 lanes: lane-position nibble tables, word (16k + n) * lanes + g =
+//                          (n << 4k) * x^(128 (lanes - 1 - g)) — lane g's weight in its group's register,
+//                          interleaved by lane so that a half-wave's lookups spread over the 32 banks
 inline int64_t byte_table_offset(int lanes) { return (int64_t)(2 + log2_lanes(lanes)) * 1024; }
-inline int64_t compact_words(int lanes) { return byte_table_offset(lanes) + 256 + 2048; }
+inline bool has_lane_tables(int lanes) { return lanes == 4 || lanes == 8; }
+inline int64_t lane_table_offset(int lanes) { return byte_table_offset(lanes) + 256 + 2048; }
+inline int64_t compact_words(int lanes) { return lane_table_offset(lanes) + (has_lane_tables(lanes) ? 128 * lanes : 0); }
 
 inline int64_t build_compact(int algo, int lanes, uint32_t* out) {
     const int levels = log2_lanes(lanes);
@@ -88,6 +93,14 @@ inline int64_t build_compact(int algo, int lanes, uint32_t* out) {
     for (uint32_t b = 0; b < 256; ++b) bt[b] = mul(algo, b, x8);
     operator_tables(algo, xpow(algo, 64), bt + 256);
     operator_tables(algo, xpow(algo, 96), bt + 256 + 1024);
+    if (has_lane_tables(lanes)) {
+        uint32_t* lt = out + lane_table_offset(lanes);
+        for (int g = 0; g < lanes; ++g) {
+            const uint32_t w = xpow(algo, 128ull * (uint64_t)(lanes - 1 - g));
+            for (int k = 0; k < 8; ++k)
+                for (uint32_t n = 0; n < 16; ++n) lt[(16 * k + (int)n) * lanes + g] = mul(algo, n << (4 * k), w);
+        }
+    }
     return compact_words(lanes);
 }
 

@@ -18,6 +18,8 @@ class KernelModel:
         self.byte = t[(2 + self.levels) * 1024:(2 + self.levels) * 1024 + 256]
         self.x64 = t[(2 + self.levels) * 1024 + 256:(2 + self.levels) * 1024 + 1280]
         self.x96 = t[(2 + self.levels) * 1024 + 1280:(2 + self.levels) * 1024 + 2304]
+        lo = (2 + self.levels) * 1024 + 2304  # lane-position nibble tables (groups of 4 / 8 lanes)
+        self.lanetab = t[lo:lo + 128 * lanes] if lanes in (4, 8) else None
 
     @staticmethod
     def _mul(tab, v: int) -> int:
@@ -80,6 +82,12 @@ class KernelModel:
                 v = self._mul(self.x32, v) ^ acc[2]
                 v = self._mul(self.x32, v) ^ acc[3]
             lane_vals.append(v)
+        if self.lanetab is not None:  # finish_lanes' lane-position products + XOR over the group
+            total = 0
+            for g, v in enumerate(lane_vals):
+                for k in range(8):
+                    total ^= int(self.lanetab[(16 * k + ((v >> (4 * k)) & 15)) * G + g])
+            return (~total) & 0xFFFFFFFF
         for s in range(self.levels):
             lane_vals = [self._mul(self.lv[s], lane_vals[2 * m]) ^ lane_vals[2 * m + 1]
                          for m in range(len(lane_vals) // 2)]

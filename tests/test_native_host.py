@@ -140,7 +140,12 @@ def test_host_tables_against_oracle(algo):
     for lanes in (4, 8, 16, 32, 64):
         t = ck.host_tables(algo, lanes)
         bo = (2 + int(np.log2(lanes))) * 1024
-        assert t.size == bo + 256 + 2048
+        assert t.size == bo + 256 + 2048 + (128 * lanes if lanes in (4, 8) else 0)
+        if lanes in (4, 8):  # lane-position nibble tables: (n << 4k) * x^(128 (lanes - 1 - g))
+            lo = bo + 2304
+            for g, k, nb in ((0, 0, 1), (lanes - 1, 7, 15), (1, 3, 9), (lanes - 2, 5, 4)):
+                want = oracle.gf_mul(algo, nb << (4 * k), oracle.xpow8n(algo, 16 * (lanes - 1 - g)))
+                assert t[lo + (16 * k + nb) * lanes + g] == want
         assert (t[bo:bo + 256] == oracle.table(algo)).all()  # ReflectedIntCrc.java:30-35
         for off, k in ((bo + 256, 8), (bo + 1280, 12)):  # x^64, x^96 operators
             assert t[off + 256 * 2 + 7] == oracle.gf_mul(algo, 7 << 16, oracle.xpow8n(algo, k))

@@ -86,7 +86,7 @@ def main(paths):
 
     small = {f"u{S}_l{G}": (S, G) for S, G in ((32, 1), (32, 4), (64, 1), (64, 4), (64, 8), (128, 1), (128, 4),
                                                (128, 8), (256, 1), (256, 4), (256, 8), (512, 1), (512, 4), (512, 8),
-                                               (1024, 8))}
+                                               (1024, 8), (2048, 8), (8192, 8), (16384, 16))}
 
     # one digest per entry of the largest batch (4 GiB of the smallest uniform size)
     out = torch.empty(max(n, max((4 << 30) // S for S, _ in small.values())), dtype=torch.int32, device=dev)
