@@ -747,7 +747,11 @@ bool is_pinned_host(const void* p) {
     return attr.type == hipMemoryTypeHost;
 }
 
-// Unsorted index or an entry larger than a segment: one device copy of the spanned bytes.
+// Unsorted index: one device copy of the spanned bytes. The buffers are allocated with hipMalloc
+// and released with hipFree: reusing stream-ordered (hipMallocAsync) allocations of this size for
+// the copy gave wrong digests from the second call on (128-512 MiB spans, both pinned and pageable
+// sources, with or without a sync after the copy; tools/diag_host_big.py, profiles/r03l_*), and
+// hipMalloc'd buffers did not.
 int host_batch_oneshot(DeviceState& ds, HostStage& hs, int algo, const uint8_t* h_base, uint64_t base_size,
                        const uint64_t* h_offsets, const uint32_t* h_lengths, uint64_t n, const uint32_t* h_seeds,
                        uint32_t seed_all, uint32_t* h_out) {
@@ -756,26 +760,27 @@ int host_batch_oneshot(DeviceState& ds, HostStage& hs, int algo, const uint8_t* 
     uint64_t* d_off = nullptr;
     uint32_t *d_len = nullptr, *d_seeds = nullptr, *d_out = nullptr;
     hipError_t e = hipSuccess;
-    if (base_size) e = hipMallocAsync((void**)&d_base, base_size, st);
-    if (e == hipSuccess) e = hipMallocAsync((void**)&d_off, n * 8, st);
-    if (e == hipSuccess) e = hipMallocAsync((void**)&d_len, n * 4, st);
-    if (e == hipSuccess) e = hipMallocAsync((void**)&d_out, n * 4, st);
-    if (e == hipSuccess && h_seeds) e = hipMallocAsync((void**)&d_seeds, n * 4, st);
-    if (e == hipSuccess && base_size) e = hipMemcpyAsync(d_base, h_base, base_size, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_off, h_offsets, n * 8, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_len, h_lengths, n * 4, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess && h_seeds) e = hipMemcpyAsync(d_seeds, h_seeds, n * 4, hipMemcpyHostToDevice, st);
+    if (base_size) e = hipMalloc((void**)&d_base, base_size);
+    if (e == hipSuccess) e = hipMalloc((void**)&d_off, n * 8);
+    if (e == hipSuccess) e = hipMalloc((void**)&d_len, n * 4);
+    if (e == hipSuccess) e = hipMalloc((void**)&d_out, n * 4);
+    if (e == hipSuccess && h_seeds) e = hipMalloc((void**)&d_seeds, n * 4);
     int rc = BKD_OK;
-    if (e != hipSuccess) rc = fail(BKD_ERR_HIP, std::string("host batch staging: ") + hipGetErrorString(e));
+    if (e != hipSuccess) rc = fail(BKD_ERR_NOMEM, std::string("host batch staging: ") + hipGetErrorString(e));
+    if (rc == BKD_OK && base_size) e = hipMemcpyAsync(d_base, h_base, base_size, hipMemcpyHostToDevice, st);
+    if (rc == BKD_OK && e == hipSuccess) e = hipMemcpyAsync(d_off, h_offsets, n * 8, hipMemcpyHostToDevice, st);
+    if (rc == BKD_OK && e == hipSuccess) e = hipMemcpyAsync(d_len, h_lengths, n * 4, hipMemcpyHostToDevice, st);
+    if (rc == BKD_OK && e == hipSuccess && h_seeds) e = hipMemcpyAsync(d_seeds, h_seeds, n * 4, hipMemcpyHostToDevice, st);
+    if (rc == BKD_OK && e != hipSuccess) rc = fail(BKD_ERR_HIP, std::string("host batch staging: ") + hipGetErrorString(e));
     if (rc == BKD_OK) rc = indexed_batch(ds, algo, d_base, base_size, d_off, d_len, n, d_seeds, seed_all, d_out, st);
     if (rc == BKD_OK) {
         e = hipMemcpyAsync(h_out, d_out, n * 4, hipMemcpyDeviceToHost, st);
         if (e != hipSuccess) rc = fail(BKD_ERR_HIP, std::string("host batch: ") + hipGetErrorString(e));
     }
-    for (void* p : {(void*)d_base, (void*)d_off, (void*)d_len, (void*)d_seeds, (void*)d_out})
-        if (p) (void)hipFreeAsync(p, st);
     e = hipStreamSynchronize(st);
     if (rc == BKD_OK && e != hipSuccess) rc = fail(BKD_ERR_HIP, std::string("host batch: ") + hipGetErrorString(e));
+    for (void* p : {(void*)d_base, (void*)d_off, (void*)d_len, (void*)d_seeds, (void*)d_out})
+        if (p) (void)hipFree(p);
     return rc;
 }
 
@@ -804,16 +809,8 @@ int host_batch_pipelined(DeviceState& ds, HostStage& hs, int algo, const uint8_t
             b1 = e1;
             ++i1;
         }
-        const uint64_t cnt = i1 - i0, span = b1 - b0;
+        const uint64_t cnt = i1 - i0, span = b1 - b0;  // span <= kSeg: longer entries arrive in pieces
         if ((rc = drain(s))) break;
-        if (span > HostStage::kSeg) {  // a single entry larger than a segment (cnt == 1, offset b0)
-            if ((rc = drain(s ^ 1))) break;
-            const uint64_t zero = 0;
-            rc = host_batch_oneshot(ds, hs, algo, h_base + b0, span, &zero, h_lengths + i0, 1,
-                                    h_seeds ? h_seeds + i0 : nullptr, seed_all, h_out + i0);
-            i0 = i1;
-            continue;
-        }
         for (uint64_t j = 0; j < cnt; ++j) {
             hs.h_off[s][j] = h_offsets[i0 + j] - b0;
             hs.h_len[s][j] = h_lengths[i0 + j];
@@ -1076,7 +1073,7 @@ int host_route() {
 }
 
 int cpu_resume(int algo, uint32_t current, const void* p, uint64_t len, uint32_t* out) {
-    *out = ~bkd::host::crc_raw(algo, ~current, (const uint8_t*)p, (size_t)len);
+    *out = ~bkd::host::fold(algo, ~current, (const uint8_t*)p, len);  // >= 4 MiB: over the host pool
     return BKD_OK;
 }
 
@@ -1343,8 +1340,43 @@ int bkd_crc_batch_host(int algo, const void* h_base, uint64_t base_size, const u
     if (rc) return rc;
     if (!sorted) return host_batch_oneshot(*ds, hs, algo, (const uint8_t*)h_base, base_size, h_offsets, h_lengths, n,
                                            h_seeds, seed_all, h_out);
-    return host_batch_pipelined(*ds, hs, algo, (const uint8_t*)h_base, h_offsets, h_lengths, n, h_seeds, seed_all,
-                                h_out);
+    uint64_t pieces = 0;
+    for (uint64_t i = 0; i < n; ++i)
+        if (h_lengths[i] > HostStage::kSeg) pieces += (h_lengths[i] + HostStage::kSeg - 1) / HostStage::kSeg - 1;
+    if (pieces == 0)
+        return host_batch_pipelined(*ds, hs, algo, (const uint8_t*)h_base, h_offsets, h_lengths, n, h_seeds, seed_all,
+                                    h_out);
+    // Entries longer than a staging segment go through the pipeline as segment-sized pieces (the
+    // first with the entry's seed, the others with seed ~0, i.e. their zero-initialised registers)
+    // and are joined here, reg = reg * x^(8 len) ^ raw, as the device plan joins its chunks.
+    const uint64_t m = n + pieces;
+    std::vector<uint64_t> off2(m);
+    std::vector<uint32_t> len2(m), seed2(m), out2(m);
+    for (uint64_t i = 0, j = 0; i < n; ++i) {
+        uint64_t o = h_offsets[i], left = h_lengths[i];
+        seed2[j] = h_seeds ? h_seeds[i] : seed_all;
+        do {
+            const uint32_t l = (uint32_t)std::min<uint64_t>(left, HostStage::kSeg);
+            off2[j] = o;
+            len2[j] = l;
+            if (o != h_offsets[i]) seed2[j] = 0xFFFFFFFFu;
+            o += l;
+            left -= l;
+            ++j;
+        } while (left);
+    }
+    rc = host_batch_pipelined(*ds, hs, algo, (const uint8_t*)h_base, off2.data(), len2.data(), m, seed2.data(), 0,
+                              out2.data());
+    if (rc) return rc;
+    const uint32_t xseg = bkd::gf2::xpow(algo, 8ull * HostStage::kSeg);
+    for (uint64_t i = 0, j = 0; i < n; ++i) {
+        uint32_t reg = ~out2[j++];
+        for (uint64_t at = HostStage::kSeg; at < h_lengths[i]; at += HostStage::kSeg, ++j)
+            reg = bkd::gf2::mul(algo, reg, len2[j] == HostStage::kSeg ? xseg : bkd::gf2::xpow(algo, 8ull * len2[j])) ^
+                  ~out2[j];
+        h_out[i] = h_lengths[i] > HostStage::kSeg ? ~reg : out2[j - 1];
+    }
+    return BKD_OK;
 }
 
 int bkd_cpu_resume(int algo, uint32_t current, const void* h_ptr, uint64_t len, uint32_t* out) {

@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <atomic>
 
+#include "crc_tables.hpp"
 #include "host_crc.hpp"
 
 namespace bkd {
@@ -58,7 +59,7 @@ Pool::~Pool() {
 
 int Pool::threads() const { return (int)workers_.size() + 1; }
 
-int Pool::active() const { return std::max(1, std::min(active_, threads())); }
+int Pool::active() const { return std::max(1, std::min(active_.load(std::memory_order_relaxed), threads())); }
 
 void Pool::set_active(int n) { active_ = n <= 0 ? threads() : std::min(n, threads()); }
 
@@ -107,7 +108,8 @@ namespace {
 constexpr uint64_t kInlineBytes = 512u << 10;
 
 // Runs body(i0, i1) over [0, n) in chunks taken from a shared counter, so ragged entry sizes
-// balance without a serial prefix sum. bytes_hint: the batch's bytes when cheaply known, else 0.
+// balance without a serial prefix sum. Batches of fewer than 4096 entries and under kInlineBytes
+// run inline.
 template <class Body>
 void for_chunks(uint64_t n, const uint32_t* lens, Body&& body) {
     if (n == 0) return;
@@ -133,6 +135,16 @@ void for_chunks(uint64_t n, const uint32_t* lens, Body&& body) {
     });
 }
 
+// Entries of at least kSplitBytes are folded in kPieceBytes pieces on the whole pool, each piece's
+// register from zero, joined by Horner with x^(8 * piece) (the device plan's join,
+// plan_kernels.hpp): a long entry is not left to one core while the others idle.
+constexpr uint64_t kPieceBytes = 1u << 20;
+constexpr uint64_t kSplitBytes = 4u << 20;
+
+inline bool split_on() { return Pool::get().active() > 1; }
+
+inline bool is_big(uint64_t len) { return len >= kSplitBytes; }
+
 inline uint32_t be32(const uint8_t* p) {
     return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
 }
@@ -151,24 +163,66 @@ inline void put_be64(uint8_t* p, uint64_t v) {
 
 }  // namespace
 
+uint32_t fold(int algo, uint32_t reg, const uint8_t* p, uint64_t len) {
+    Pool& pool = Pool::get();
+    const int threads = pool.active();
+    if (threads == 1 || !is_big(len)) return crc_raw(algo, reg, p, (size_t)len);
+    const uint64_t np = (len + kPieceBytes - 1) / kPieceBytes;
+    std::vector<uint32_t> raw(np);
+    std::atomic<uint64_t> next{0};
+    pool.run((int)std::min<uint64_t>((uint64_t)threads, np), [&](int) {
+        for (;;) {
+            const uint64_t k = next.fetch_add(1, std::memory_order_relaxed);
+            if (k >= np) return;
+            const uint64_t at = k * kPieceBytes;
+            raw[k] = crc_raw(algo, k == 0 ? reg : 0u, p + at, (size_t)std::min(kPieceBytes, len - at));
+        }
+    });
+    const uint32_t xp = gf2::xpow(algo, 8ull * kPieceBytes);
+    uint32_t r = raw[0];
+    for (uint64_t k = 1; k < np; ++k) {
+        const uint64_t l = std::min(kPieceBytes, len - k * kPieceBytes);
+        r = gf2::mul(algo, r, l == kPieceBytes ? xp : gf2::xpow(algo, 8ull * l)) ^ raw[k];
+    }
+    return r;
+}
+
 void crc_list(int algo, const uint8_t* const* ptrs, const uint32_t* lens, uint64_t n, const uint32_t* seeds,
               uint32_t seed_all, uint32_t* out) {
+    const bool split = split_on();
+    std::atomic<bool> big{false};
     for_chunks(n, lens, [&](uint64_t i0, uint64_t i1) {
         for (uint64_t i = i0; i < i1; ++i) {
+            if (split && is_big(lens[i])) {
+                big.store(true, std::memory_order_relaxed);
+                continue;
+            }
             const uint32_t seed = seeds ? seeds[i] : seed_all;
             out[i] = lens[i] ? ~crc_raw(algo, ~seed, ptrs[i], lens[i]) : seed;
         }
     });
+    if (big.load())
+        for (uint64_t i = 0; i < n; ++i)
+            if (is_big(lens[i])) out[i] = ~fold(algo, ~(seeds ? seeds[i] : seed_all), ptrs[i], lens[i]);
 }
 
 void crc_indexed(int algo, const uint8_t* base, const uint64_t* offsets, const uint32_t* lens, uint64_t n,
                  const uint32_t* seeds, uint32_t seed_all, uint32_t* out) {
+    const bool split = split_on();
+    std::atomic<bool> big{false};
     for_chunks(n, lens, [&](uint64_t i0, uint64_t i1) {
         for (uint64_t i = i0; i < i1; ++i) {
+            if (split && is_big(lens[i])) {
+                big.store(true, std::memory_order_relaxed);
+                continue;
+            }
             const uint32_t seed = seeds ? seeds[i] : seed_all;
             out[i] = lens[i] ? ~crc_raw(algo, ~seed, base + offsets[i], lens[i]) : seed;
         }
     });
+    if (big.load())
+        for (uint64_t i = 0; i < n; ++i)
+            if (is_big(lens[i])) out[i] = ~fold(algo, ~(seeds ? seeds[i] : seed_all), base + offsets[i], lens[i]);
 }
 
 // DigestManager.verifyDigest ($BK/proto/checksum/DigestManager.java:226-283), in its order: too
@@ -177,35 +231,49 @@ void crc_indexed(int algo, const uint8_t* base, const uint64_t* offsets, const u
 uint64_t verify_frames(int algo, int64_t ledger_id, int64_t first_entry_id, int id_checks,
                        const uint8_t* const* frames, const uint32_t* lens, uint64_t n, int32_t* status) {
     const uint32_t mac = algo == 0 ? 4u : 8u;
+    const bool split = split_on();
+    std::atomic<bool> big{false};
+    auto one = [&](uint64_t i, bool whole_pool) -> int32_t {
+        const uint32_t l = lens[i];
+        if (l < 32u + mac) return 1;
+        const uint8_t* f = frames[i];
+        uint32_t reg = crc_raw(algo, 0xFFFFFFFFu, f, 32);  // update(0, header)
+        reg = whole_pool ? fold(algo, reg, f + 32 + mac, l - 32u - mac) : crc_raw(algo, reg, f + 32 + mac, l - 32u - mac);
+        const uint32_t computed = ~reg;
+        const uint32_t hi = mac == 8u ? be32(f + 32) : 0u;
+        const uint32_t expect = be32(f + 32 + (mac - 4u));
+        const int64_t lid = (int64_t)(((uint64_t)be32(f) << 32) | be32(f + 4));
+        const int64_t eid = (int64_t)(((uint64_t)be32(f + 8) << 32) | be32(f + 12));
+        if (hi != 0u || computed != expect) return 2;
+        if (id_checks < 2 && lid != ledger_id) return 3;
+        if (id_checks == 0 && eid != first_entry_id + (int64_t)i) return 4;
+        return 0;
+    };
     std::atomic<uint64_t> first_bad{n};
-    for_chunks(n, lens, [&](uint64_t i0, uint64_t i1) {
-        uint64_t bad = n;
-        for (uint64_t i = i0; i < i1; ++i) {
-            const uint32_t l = lens[i];
-            int32_t st;
-            if (l < 32u + mac) {
-                st = 1;
-            } else {
-                const uint8_t* f = frames[i];
-                uint32_t reg = crc_raw(algo, 0xFFFFFFFFu, f, 32);  // update(0, header)
-                reg = crc_raw(algo, reg, f + 32 + mac, l - 32u - mac);
-                const uint32_t computed = ~reg;
-                const uint32_t hi = mac == 8u ? be32(f + 32) : 0u;
-                const uint32_t expect = be32(f + 32 + (mac - 4u));
-                const int64_t lid = (int64_t)(((uint64_t)be32(f) << 32) | be32(f + 4));
-                const int64_t eid = (int64_t)(((uint64_t)be32(f + 8) << 32) | be32(f + 12));
-                if (hi != 0u || computed != expect) st = 2;
-                else if (id_checks < 2 && lid != ledger_id) st = 3;
-                else if (id_checks == 0 && eid != first_entry_id + (int64_t)i) st = 4;
-                else st = 0;
-            }
-            status[i] = st;
-            if (st != 0 && i < bad) bad = i;
-        }
+    auto note_bad = [&](uint64_t bad) {
         uint64_t cur = first_bad.load(std::memory_order_relaxed);
         while (bad < cur && !first_bad.compare_exchange_weak(cur, bad, std::memory_order_relaxed)) {
         }
+    };
+    for_chunks(n, lens, [&](uint64_t i0, uint64_t i1) {
+        uint64_t bad = n;
+        for (uint64_t i = i0; i < i1; ++i) {
+            if (split && is_big(lens[i])) {
+                big.store(true, std::memory_order_relaxed);
+                continue;
+            }
+            const int32_t st = one(i, false);
+            status[i] = st;
+            if (st != 0 && i < bad) bad = i;
+        }
+        note_bad(bad);
     });
+    if (big.load())
+        for (uint64_t i = 0; i < n; ++i)
+            if (is_big(lens[i])) {
+                status[i] = one(i, true);
+                if (status[i] != 0) note_bad(i);
+            }
     return first_bad.load();
 }
 
@@ -216,21 +284,33 @@ void package_frames(int algo, int64_t ledger_id, const int64_t* entry_ids, const
                     const int64_t* length_fields, const uint8_t* const* payloads, const uint32_t* lens, uint64_t n,
                     uint8_t* frames, uint64_t stride, uint32_t* digests) {
     const uint32_t mac = algo == 0 ? 4u : 8u;
+    const bool split = split_on();
+    std::atomic<bool> big{false};
+    auto one = [&](uint64_t i, bool whole_pool) {
+        uint8_t* f = frames + i * stride;
+        put_be64(f, (uint64_t)ledger_id);
+        put_be64(f + 8, (uint64_t)entry_ids[i]);
+        put_be64(f + 16, (uint64_t)lacs[i]);
+        put_be64(f + 24, (uint64_t)length_fields[i]);
+        uint32_t reg = crc_raw(algo, 0xFFFFFFFFu, f, 32);
+        if (lens[i]) reg = whole_pool ? fold(algo, reg, payloads[i], lens[i]) : crc_raw(algo, reg, payloads[i], lens[i]);
+        const uint32_t d = ~reg;
+        if (mac == 8u) put_be32(f + 32, 0u);
+        put_be32(f + 32 + (mac - 4u), d);
+        digests[i] = d;
+    };
     for_chunks(n, lens, [&](uint64_t i0, uint64_t i1) {
         for (uint64_t i = i0; i < i1; ++i) {
-            uint8_t* f = frames + i * stride;
-            put_be64(f, (uint64_t)ledger_id);
-            put_be64(f + 8, (uint64_t)entry_ids[i]);
-            put_be64(f + 16, (uint64_t)lacs[i]);
-            put_be64(f + 24, (uint64_t)length_fields[i]);
-            uint32_t reg = crc_raw(algo, 0xFFFFFFFFu, f, 32);
-            if (lens[i]) reg = crc_raw(algo, reg, payloads[i], lens[i]);
-            const uint32_t d = ~reg;
-            if (mac == 8u) put_be32(f + 32, 0u);
-            put_be32(f + 32 + (mac - 4u), d);
-            digests[i] = d;
+            if (split && is_big(lens[i])) {
+                big.store(true, std::memory_order_relaxed);
+                continue;
+            }
+            one(i, false);
         }
     });
+    if (big.load())
+        for (uint64_t i = 0; i < n; ++i)
+            if (is_big(lens[i])) one(i, true);
 }
 
 }  // namespace host

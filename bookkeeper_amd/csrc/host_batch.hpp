@@ -11,6 +11,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -42,12 +43,16 @@ class Pool {
     std::mutex mu_, call_mu_;
     std::condition_variable cv_, done_;
     const std::function<void(int)>* job_ = nullptr;
-    int parts_ = 0, pending_ = 0, active_ = 0;
+    int parts_ = 0, pending_ = 0;
+    std::atomic<int> active_{0};  // set_active() may run while other threads submit work
     uint64_t gen_ = 0;
     bool stop_ = false;
 };
 
 // ---- the CPU route of host-resident batches (semantics of include/bkdigest.h) ----
+// The register after folding p[0, len) onto reg; from 4 MiB on in 1 MiB pieces over the pool,
+// joined with x^(8 * piece) (one long buffer uses every core, not one).
+uint32_t fold(int algo, uint32_t reg, const uint8_t* p, uint64_t len);
 // out[i] = resume(seed_i, entry i): entry i at ptrs[i] (list) or base + offsets[i] (indexed).
 void crc_list(int algo, const uint8_t* const* ptrs, const uint32_t* lens, uint64_t n, const uint32_t* seeds,
               uint32_t seed_all, uint32_t* out);

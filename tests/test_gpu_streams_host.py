@@ -1,6 +1,7 @@
 """GPU: per-stream bounds reporting, stream-ordered per-call resumes, the CPU/GPU per-call routes,
 and the host-resident DigestManager batches (BatchedReadOp / PendingAddOp with entries in host
 memory), all bit-exact against the oracle."""
+import ctypes
 import threading
 
 import numpy as np
@@ -480,3 +481,36 @@ def test_host_release_frees_idle_staging_and_restarts(gpu):
             for i in range(0, len(frames), 37):
                 assert bytes(hdrs[i]) == bytes(frames[i][:36])
             ck.host_release()
+
+
+@pytest.mark.parametrize("algo", [ck.CRC32C, ck.CRC32])
+def test_long_host_entries_gpu_route_repeated(gpu, algo):
+    """Host entries longer than a staging segment (64 MiB) through the GPU route: cut into pieces,
+    pipelined and joined on the host; an unsorted index takes the one-copy route. Each call is
+    repeated — the one-copy route once reused stream-ordered allocations and went wrong from the
+    second call on (profiles/r03l_*). The per-call resume of a 150 MiB buffer on the GPU route too."""
+    M = 1 << 20
+    rng = np.random.default_rng(60 + algo)
+    host = np.frombuffer(rng.bytes(200 * M), dtype=np.uint8)
+    offs = np.array([0, 5, 64 * M + 9, 150 * M], np.uint64)
+    lens = np.array([3, 64 * M + 1, 85 * M + 3, 50 * M], np.uint32)
+    seeds = rng.integers(0, 2**32, offs.size, dtype=np.uint64).astype(np.uint32)
+    want = np.array([ck.cpu_resume(algo, int(s), host[int(o):int(o) + int(l)]) & 0xFFFFFFFF
+                     for o, l, s in zip(offs, lens, seeds)], np.uint32)
+    with ck.host_batch_route(ck.HOST_ROUTE_GPU):
+        for _ in range(3):
+            assert (ck.crc_batch_host(algo, host, offs, lens, seeds=seeds) == want).all()
+            perm = np.array([2, 0, 3, 1])  # unsorted: the one-copy route
+            assert (ck.crc_batch_host(algo, host, offs[perm], lens[perm], seeds=seeds[perm]) == want[perm]).all()
+        old = ck.get_cpu_route_max()
+        ck.set_cpu_route_max(0)
+        try:
+            buf = host[7:7 + 150 * M]
+            w = ck.cpu_resume(algo, 0xABCD, buf) & 0xFFFFFFFF
+            for _ in range(2):
+                out = ctypes.c_uint32(0)
+                assert lib().bkd_resume_host(algo, 0xABCD, ctypes.c_void_p(buf.ctypes.data), ctypes.c_uint64(buf.size),
+                                             ctypes.byref(out)) == 0
+                assert out.value == w
+        finally:
+            ck.set_cpu_route_max(old)

@@ -133,3 +133,36 @@ def test_survey_framing_vectors_through_cpu_package():
         payload = (np.arange(size) & 0xFF).astype(np.uint8)
         _, digests = dm.package_batch_host(np.array([1]), np.array([0]), np.array([size]), [payload])
         assert digests[0] == d, (algo, size)
+
+
+@pytest.mark.parametrize("algo,dtype", [(ck.CRC32C, dg.DigestType.CRC32C), (ck.CRC32, dg.DigestType.CRC32)])
+def test_long_entries_fold_over_the_pool(algo, dtype):
+    """Entries of >= 4 MiB are folded in 1 MiB pieces over the pool and joined with x^(8 * piece)
+    (host_batch.cpp fold): lengths at and around the split and piece boundaries, seeded, mixed with
+    short entries; the per-call CPU resume, a long verified frame (and one corrupted in its last
+    piece) and a long packaged payload — all against the oracle."""
+    rng = np.random.default_rng(51 + algo)
+    size = 24 << 20
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    M = 1 << 20
+    lens = np.array([4 * M, 4 * M - 1, 4 * M + 1, 9 * M + M // 2 + 3, M + 7, 0, 100, 5 * M], np.uint32)
+    offs = rng.integers(0, size - int(lens.max()), lens.size).astype(np.uint64)
+    seeds = rng.integers(0, 2**32, lens.size, dtype=np.uint64).astype(np.uint32)
+    got = ck.crc_batch_host(algo, host, offs, lens, seeds=seeds)
+    assert (got == oracle.batch(algo, host, offs.astype(np.int64), lens, seeds=seeds)).all()
+    buf = host[3:3 + 9 * M + 5]
+    assert ck.cpu_resume(algo, 0x5EED, buf) & 0xFFFFFFFF == oracle.resume(algo, 0x5EED, buf.tobytes())
+    ledger, first = 7, 40
+    dm = dg.DigestManager.instantiate(ledger, b"", dtype)
+    payload = host[11:11 + 5 * M + 13]
+    d, hdr = oracle.digest_entry(algo, ledger, first, first - 1, payload.size, payload.tobytes())
+    frame = bytearray(hdr + oracle.digest_bytes(algo, d) + payload.tobytes())
+    short = bytearray(frame[:32 + dm.macCodeLength] + b"")  # header + digest, empty payload: bad digest
+    st, fb = dm.verify_batch_host([frame, short], first)
+    assert st[0] == 0 and fb == 1
+    frame[-2] ^= 0x10
+    st, fb = dm.verify_batch_host([frame], first)
+    assert st[0] == 2 and fb == 0
+    frames, digests = dm.package_batch_host(np.array([first]), np.array([first - 1]), np.array([payload.size]),
+                                            [payload])
+    assert digests[0] == d and bytes(frames[0, :32]) == hdr
