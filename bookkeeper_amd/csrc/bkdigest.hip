@@ -54,11 +54,13 @@ int lane_index(int lanes) {
     return -1;
 }
 
-// Stream-ordered scratch kept per (device, stream) between calls. A call's kernels use it in
-// stream order, so consecutive calls on one stream can share it; the launch sequence is enqueued
-// under `mu` so that host threads sharing a stream do not interleave their sequences. It only
-// grows (old buffer released with hipFreeAsync on the same stream). Per-call hipMallocAsync /
-// hipFreeAsync left the GPU idle ~40 us between calls (profiles/r01_diag_ragged.log).
+// Scratch kept per (device, stream) between calls. A call's kernels use it in stream order, so
+// consecutive calls on one stream can share it; the launch sequence is enqueued under `mu` so that
+// host threads sharing a stream do not interleave their sequences. It only grows: the old buffer is
+// freed after a sync of its stream (growth is rare; per-call allocation left the GPU idle ~40 us
+// between calls, profiles/r01_diag_ragged.log). Plain hipMalloc, not the stream-ordered pool:
+// reused hipMallocAsync blocks fed stale data to the kernels on the host one-copy route (round 3,
+// DESIGN.md §5a), so the library keeps no device memory of its own in that pool.
 struct StreamScratch {
     std::recursive_mutex mu;
     uint8_t* buf[3] = {};  // slot 0: plan scratch (launch_plan), 1: verify pipeline, 2: segment CRCs
@@ -77,7 +79,7 @@ struct StreamScratch {
     uint32_t vepoch = 0;
     hipError_t vflag_word(hipStream_t st, uint32_t** out) {
         if (!vflag) {
-            hipError_t e = hipMallocAsync((void**)&vflag, sizeof(uint32_t), st);
+            hipError_t e = hipMalloc((void**)&vflag, sizeof(uint32_t));
             if (e == hipSuccess) e = hipMemsetAsync(vflag, 0, sizeof(uint32_t), st);
             if (e != hipSuccess) {
                 vflag = nullptr;
@@ -89,7 +91,7 @@ struct StreamScratch {
     }
     hipError_t run_word(hipStream_t st, uint32_t** out) {
         if (!run) {
-            hipError_t e = hipMallocAsync((void**)&run, sizeof(uint32_t), st);
+            hipError_t e = hipMalloc((void**)&run, sizeof(uint32_t));
             if (e == hipSuccess) e = hipMemsetAsync(run, 0, sizeof(uint32_t), st);
             if (e != hipSuccess) {
                 run = nullptr;
@@ -101,7 +103,7 @@ struct StreamScratch {
     }
     hipError_t uni_word(hipStream_t st, uint32_t** out) {
         if (!uni) {
-            hipError_t e = hipMallocAsync((void**)&uni, sizeof(uint32_t), st);
+            hipError_t e = hipMalloc((void**)&uni, sizeof(uint32_t));
             if (e == hipSuccess) e = hipMemsetAsync(uni, 0, sizeof(uint32_t), st);
             if (e != hipSuccess) {
                 uni = nullptr;
@@ -113,7 +115,7 @@ struct StreamScratch {
     }
     hipError_t flag(hipStream_t st, uint32_t** out) {
         if (!err) {
-            hipError_t e = hipMallocAsync((void**)&err, sizeof(uint32_t), st);
+            hipError_t e = hipMalloc((void**)&err, sizeof(uint32_t));
             if (e == hipSuccess) e = hipMemsetAsync(err, 0, sizeof(uint32_t), st);
             if (e == hipSuccess && !h_err) e = hipHostMalloc((void**)&h_err, sizeof(uint32_t), hipHostMallocDefault);
             if (e != hipSuccess) {
@@ -127,11 +129,15 @@ struct StreamScratch {
     // Returns slot `which` with at least `bytes` bytes, stream-ordered on `st`.
     hipError_t get(int which, size_t bytes, hipStream_t st, uint8_t** out) {
         if (cap[which] < bytes) {
-            if (buf[which]) (void)hipFreeAsync(buf[which], st);
+            if (buf[which]) {  // work already enqueued on this stream may still use the old buffer
+                const hipError_t e = hipStreamSynchronize(st);
+                if (e != hipSuccess) return e;
+                (void)hipFree(buf[which]);
+            }
             buf[which] = nullptr;
             cap[which] = 0;
             const size_t want = bytes + bytes / 4 + 4096;
-            hipError_t e = hipMallocAsync((void**)&buf[which], want, st);
+            hipError_t e = hipMalloc((void**)&buf[which], want);
             if (e != hipSuccess) return e;
             cap[which] = want;
         }
@@ -262,12 +268,6 @@ int init_device_locked(int dev) {
         BKD_HIP(hipMalloc(&ds.xinv[algo], sizeof(inv)));
         BKD_HIP(hipMemcpy(ds.xinv[algo], inv, sizeof(inv), hipMemcpyHostToDevice));
     }
-    // stream-ordered scratch for the plan: keep freed blocks in the pool between calls
-    hipMemPool_t pool;
-    if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-        uint64_t thr = UINT64_MAX;
-        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
-    }
     BKD_HIP(hipSetDevice(prev));
     ds.ready.store(true, std::memory_order_release);
     return BKD_OK;
@@ -350,6 +350,11 @@ int auto_lanes(uint64_t mean_len, uint64_t n = UINT64_MAX, int cus = 256) {
 #endif
 #ifndef BKD_NT
 #define BKD_NT 1
+#endif
+#ifndef BKD_PACKAGE_DIGEST_PASS
+// 1: package digests written into the frames by their own kernel; 0: by the payload groups
+// (PackageSrc), which measured 3 % slower on 1M x 4 KiB (profiles/r03m_ab_order*.log)
+#define BKD_PACKAGE_DIGEST_PASS 1
 #endif
 constexpr int kPF = BKD_PF;
 constexpr bool kNT = BKD_NT != 0;
@@ -852,8 +857,8 @@ int host_batch_pipelined(DeviceState& ds, HostStage& hs, int algo, const uint8_t
 // entry points -------------------------------------------------------------------------------
 
 // Package: header kernel (32 B BE header, header CRC as the payload's seed) -> payload CRCs through
-// the direct kernel -> digest kernel (BE digest after the header). Out-of-range payload entries
-// raise the stream's bounds flag.
+// the direct kernel -> digest kernel (BE digest after the header; BKD_PACKAGE_DIGEST_PASS=0 has the
+// payload groups store it instead). Out-of-range payload entries raise the stream's bounds flag.
 int package_framed(DeviceState& ds, hipStream_t st, int algo, int64_t ledger_id, const int64_t* d_entry_ids,
                    const int64_t* d_lacs, const int64_t* d_length_fields, const void* d_payload,
                    uint64_t payload_size, const uint64_t* d_offsets, const uint32_t* d_lengths, uint64_t n,
@@ -873,6 +878,7 @@ int package_framed(DeviceState& ds, hipStream_t st, int algo, int64_t ledger_id,
     hipLaunchKernelGGL(bkd::package_header_kernel, dim3(hblocks), dim3(1024), 0, st, tab + 1024, ledger_id, d_entry_ids,
                        d_lacs, d_length_fields, n, (uint8_t*)d_frames, frame_stride, d_digests);
     BKD_HIP(hipGetLastError());
+#if BKD_PACKAGE_DIGEST_PASS
     bkd::IndexedSrc src{n, d_offsets, d_lengths, d_digests, 0u, payload_size, d_digests};
     int rc = dispatch_lanes(ds, lanes, algo, (const uint8_t*)d_payload, src, n, st, err);
     if (rc) return rc;
@@ -880,6 +886,13 @@ int package_framed(DeviceState& ds, hipStream_t st, int algo, int64_t ledger_id,
                        (uint8_t*)d_frames, frame_stride, mac);
     BKD_HIP(hipGetLastError());
     return BKD_OK;
+#else
+    // the payload groups write each frame's digest field themselves (PackageSrc)
+    (void)blocks;
+    bkd::PackageSrc src{{n, d_offsets, d_lengths, d_digests, 0u, payload_size, d_digests}, (uint8_t*)d_frames,
+                        frame_stride, mac};
+    return dispatch_lanes(ds, lanes, algo, (const uint8_t*)d_payload, src, n, st, err);
+#endif
 }
 
 // Fused verify of near-uniform frames: one kernel per lane count (crc_verify_fused_kernel).
@@ -1063,13 +1076,21 @@ int cpu_route_min_threads() {
 }
 
 // 1 = CPU, 2 = GPU, < 0 = error (a GPU route forced without a device).
-int host_route() {
+// oversize: the batch holds an entry longer than a staging segment, which the framed GPU route
+// refuses; the automatic route then takes the CPU (the provider never fails where it can compute).
+int host_route(bool oversize = false) {
     const int r = g_host_route.load(std::memory_order_relaxed);
-    if (r == 1) return 1;
+    if (r == 1 || (r == 0 && oversize)) return 1;
     if (visible_devices() <= 0)  // the provider never fails for lack of a device
         return r == 2 ? fail(BKD_ERR_NO_DEVICE, "no HIP device (host batch route forced to the GPU)") : 1;
     if (r == 2) return 2;
     return bkd::host::Pool::get().active() >= cpu_route_min_threads() ? 1 : 2;
+}
+
+bool any_longer(const uint32_t* lengths, uint64_t n, uint64_t limit) {
+    for (uint64_t i = 0; i < n; ++i)
+        if (lengths[i] > limit) return true;
+    return false;
 }
 
 int cpu_resume(int algo, uint32_t current, const void* p, uint64_t len, uint32_t* out) {
@@ -1301,12 +1322,11 @@ int bkd_stream_release(void* stream) {
             BKD_HIP(hipMemcpy(sc->h_err, sc->err, sizeof(uint32_t), hipMemcpyDeviceToHost));
             if (*sc->h_err) status = fail(BKD_ERR_BOUNDS, "an indexed entry exceeded its base buffer (entries skipped, out = 0)");
         }
-        // stream-ordered allocations go back the way they came
+        BKD_HIP(hipStreamSynchronize(st));  // the stream's own work is done with them
         for (int k = 0; k < 3; ++k)
-            if (sc->buf[k]) BKD_HIP(hipFreeAsync(sc->buf[k], st));
+            if (sc->buf[k]) BKD_HIP(hipFree(sc->buf[k]));
         for (uint32_t* w : {sc->err, sc->run, sc->uni, sc->vflag})
-            if (w) BKD_HIP(hipFreeAsync(w, st));
-        BKD_HIP(hipStreamSynchronize(st));
+            if (w) BKD_HIP(hipFree(w));
         if (sc->h_err) BKD_HIP(hipHostFree(sc->h_err));
     }
     return status;
@@ -1577,7 +1597,7 @@ int bkd_digest_verify_batch_host(int algo, int64_t ledger_id, int64_t first_entr
     if (!h_frames || !h_lengths || !h_status) return fail(BKD_ERR_INVALID_ARG, "null buffer");
     for (uint64_t i = 0; i < n; ++i)
         if (h_lengths[i] && !h_frames[i]) return fail(BKD_ERR_INVALID_ARG, "null frame " + std::to_string(i));
-    const int route = host_route();
+    const int route = host_route(any_longer(h_lengths, n, HostStage::kSeg));
     if (route < 0) return route;
     if (route == 1) {
         *h_first_bad = bkd::host::verify_frames(algo, ledger_id, first_entry_id, skip_entry_check ? 1 : 0,
@@ -1628,7 +1648,7 @@ int bkd_digest_package_batch_host(int algo, int64_t ledger_id, const int64_t* h_
         return fail(BKD_ERR_INVALID_ARG, "frame_stride must be in [32 + digest length, 4096]");
     for (uint64_t i = 0; i < n; ++i)
         if (h_lengths[i] && !h_payloads[i]) return fail(BKD_ERR_INVALID_ARG, "null payload " + std::to_string(i));
-    const int route = host_route();
+    const int route = host_route(any_longer(h_lengths, n, HostStage::kSeg));
     if (route < 0) return route;
     if (route == 1) {
         bkd::host::package_frames(algo, ledger_id, h_entry_ids, h_lacs, h_length_fields,

@@ -205,6 +205,43 @@ struct IndexedSrc {
     }
 };
 
+// The digest field of a packaged frame (f = frame + 32): the BE digest, after a zero high word for
+// CRC32's 8-byte digest (CRC32CDigestManager.java:44-46 writeInt, CRC32DigestManager.java:60-63
+// writeLong); dword stores when f is 4-byte aligned, bytes otherwise.
+__device__ __forceinline__ void put_frame_digest(uint8_t* f, uint32_t digest, uint32_t mac) {
+    const uint32_t be = __builtin_bswap32(digest);
+    if ((((uintptr_t)f) & 3u) == 0) {
+        uint32_t* d = reinterpret_cast<uint32_t*>(f);
+        if (mac == 8) *d++ = 0u;
+        *d = be;
+    } else {
+        if (mac == 8) {
+            f[0] = f[1] = f[2] = f[3] = 0;
+            f += 4;
+        }
+        for (int k = 0; k < 4; ++k) f[k] = (uint8_t)(be >> (8 * k));
+    }
+}
+
+// Package payloads: IndexedSrc whose results (seeded with the header CRCs) are also written into
+// each frame's digest field by the group that computed them (the BKD_PACKAGE_DIGEST_PASS=0 build:
+// 3 % slower than the separate digest pass).
+struct PackageSrc : IndexedSrc {
+    uint8_t* frames;
+    uint64_t stride;
+    uint32_t mac;
+};
+
+// Where a work item's result goes: *dst, and for package payloads the frame's digest field too.
+template <class Src>
+__device__ __forceinline__ void put_result(const Src&, uint64_t, const Work& w, uint32_t v) {
+    *w.dst = v;
+}
+__device__ __forceinline__ void put_result(const PackageSrc& src, uint64_t i, const Work& w, uint32_t v) {
+    *w.dst = v;
+    put_frame_digest(src.frames + i * src.stride + 32, v, src.mac);
+}
+
 // Framed entry [32 B header][mac][payload]: CRC the payload resuming from the header CRC
 // already stored in seeds[i] (DigestManager.java:236-239); result over seeds[i] in place.
 struct FramedPayloadSrc {
@@ -496,7 +533,7 @@ __device__ __forceinline__ void groups_loop(const uint32_t* lds, uint32_t lanere
         const int st = src.get(i, wk);
         if (st != 0) {
             if (g == 0 && st != 3) {
-                *wk.dst = 0u;
+                put_result(src, i, wk, 0u);
                 if (st == 2 && err) atomicOr(err, 1u);
             }
             continue;
@@ -507,14 +544,14 @@ __device__ __forceinline__ void groups_loop(const uint32_t* lds, uint32_t lanere
                 const uint8_t* q = base + wk.s;
                 for (uint32_t k = 0; k < wk.len; ++k)
                     r = lds_word(lds, Gm::kByteTabOff + (((r ^ q[k]) & 0xffu) << 2)) ^ (r >> 8);
-                *wk.dst = r ^ wk.xorout;
+                put_result(src, i, wk, r ^ wk.xorout);
             }
             continue;
         }
         const uint32_t v =
             fold_range<G, PF, NT, false, BKD_TAIL_UNCOND != 0 || std::is_same<Src, UniformLongSrc>::value>(
                 lds, lanereg, g, base, wk.s, wk.s + (int64_t)wk.len, wk.r0);
-        if (g == 0) *wk.dst = v ^ wk.xorout;
+        if (g == 0) put_result(src, i, wk, v ^ wk.xorout);
     }
 }
 
@@ -1167,19 +1204,7 @@ __global__ void __launch_bounds__(256) package_digest_kernel(const uint32_t* __r
                                                              uint32_t mac) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    uint8_t* f = frames + i * frame_stride + 32;
-    const uint32_t be = __builtin_bswap32(digests[i]);
-    if ((((uintptr_t)f) & 3u) == 0) {
-        uint32_t* d = reinterpret_cast<uint32_t*>(f);
-        if (mac == 8) *d++ = 0u;
-        *d = be;
-    } else {
-        if (mac == 8) {
-            f[0] = f[1] = f[2] = f[3] = 0;
-            f += 4;
-        }
-        for (int k = 0; k < 4; ++k) f[k] = (uint8_t)(be >> (8 * k));
-    }
+    put_frame_digest(frames + i * frame_stride + 32, digests[i], mac);
 }
 
 // Verify step 1 (one thread per framed entry [32 B header][mac][payload], DigestManager.java:226-283):

@@ -514,3 +514,28 @@ def test_long_host_entries_gpu_route_repeated(gpu, algo):
                 assert out.value == w
         finally:
             ck.set_cpu_route_max(old)
+
+
+def test_oversize_frames_take_the_cpu_route_when_automatic(gpu):
+    """A framed host batch holding a frame longer than a staging segment (64 MiB): the automatic route
+    verifies / packages it on the CPU even where it would pick the GPU (one host thread); the route
+    forced to the GPU refuses it (BKD_ERR_INVALID_ARG), never a wrong status."""
+    M = 1 << 20
+    rng = np.random.default_rng(77)
+    payload = np.frombuffer(rng.bytes(65 * M + 3), dtype=np.uint8)
+    dm = dg.DigestManager.instantiate(5, b"", dg.DigestType.CRC32C)
+    d, hdr = oracle.digest_entry(ck.CRC32C, 5, 9, 8, payload.size, payload.tobytes())
+    frame = bytearray(hdr + oracle.digest_bytes(ck.CRC32C, d) + payload.tobytes())
+    small = bytearray(frame[:40])  # header + digest of the long frame, no payload: digest mismatch
+    ck.set_host_threads(1)
+    try:
+        with ck.host_batch_route(ck.HOST_ROUTE_AUTO):
+            st, fb = dm.verify_batch_host([frame, small], 9, skip_entry_check=True)
+            assert st.tolist() == [0, 2] and fb == 1
+            frames, digests = dm.package_batch_host(np.array([9]), np.array([8]), np.array([payload.size]), [payload])
+            assert digests[0] == d and bytes(frames[0, :32]) == hdr
+        with ck.host_batch_route(ck.HOST_ROUTE_GPU):
+            with pytest.raises(BkdError):
+                dm.verify_batch_host([frame], 9)
+    finally:
+        ck.set_host_threads(0)
