@@ -31,8 +31,11 @@ def main() -> None:
     ck.set_plan_small(0)
     reps = 10
     for J in [int(x) for x in os.environ.get("HEADS_J", "1 2 3 4 6 8 12 16 24 32").split()]:
-        lens = rng.integers(128 * J - 100, 128 * J - 20, n).astype(np.int64)
-        lens = np.maximum(lens, 17)
+        if os.environ.get("HEADS_ALIGN"):  # whole 128-byte steps, packed: every head line-aligned, no pad
+            lens = np.full(n, 128 * J, dtype=np.int64)
+        else:
+            lens = rng.integers(128 * J - 100, 128 * J - 20, n).astype(np.int64)
+            lens = np.maximum(lens, 17)
         lens[-1] = 60000
         offs = np.zeros(n, dtype=np.int64)
         np.cumsum(lens[:-1], out=offs[1:])
@@ -44,22 +47,33 @@ def main() -> None:
         out = torch.empty(n, dtype=torch.int32, device=dev)
         res = {}
         for mode in [int(m) for m in os.environ.get("HEADS_MODES", "2 1").split()]:
-            ck.set_plan_mode(mode)
+            if mode == 3:  # the uniform kernel on the same bytes (aligned runs only: every entry 128 J)
+                if not os.environ.get("HEADS_ALIGN"):
+                    continue
+                ck.set_group_lanes(8)
+                call = lambda: ck.crc_batch_uniform(ck.CRC32C, base, 128 * J, n - 1, out=out, stream=st)
+            else:
+                ck.set_plan_mode(mode)
+                call = lambda: ck.crc_batch(ck.CRC32C, base, d_off, d_len, out=out, stream=st)
             for _ in range(3):
-                ck.crc_batch(ck.CRC32C, base, d_off, d_len, out=out, stream=st)
+                call()
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(st)
             for _ in range(reps):
-                ck.crc_batch(ck.CRC32C, base, d_off, d_len, out=out, stream=st)
+                call()
             b.record(st)
             torch.cuda.synchronize()
             t = a.elapsed_time(b) / 1e3 / reps
+            ck.set_group_lanes(0)
             res[mode] = out.clone()
-            print(json.dumps({"J": J, "mode": "plan" if mode == 2 else "direct", "n": n, "mean_len": float(lens[:-1].mean()),
+            print(json.dumps({"J": J, "mode": {1: "direct", 2: "plan", 3: "uniform"}[mode], "n": n,
+                              "aligned": bool(os.environ.get("HEADS_ALIGN")), "mean_len": float(lens[:-1].mean()),
                               "ms": round(t * 1e3, 4), "GB_s": round(total / t / 1e9, 1),
                               "us_per_round": round(t * 1e6 / (n / groups), 3)}), flush=True)
         if 1 in res and 2 in res:
             assert torch.equal(res[1], res[2]), J
+        if 3 in res and 2 in res:
+            assert torch.equal(res[3][:n - 1], res[2][:n - 1]), J
         del base, d_off, d_len, out
         torch.cuda.empty_cache()
     ck.set_plan_mode(0)
