@@ -567,14 +567,16 @@ struct SmallGeo {
     int kind;  // indexed entries: 0 fold, 1 shorter than 16 B (serial), 2 out of bounds, 3 the plan's, 4 none
 };
 
-template <int G>
+// SEEDS: per-entry seeds (src.seeds != nullptr); without, no load sits under a branch in the loop
+template <int G, bool SEEDS = true>
 __device__ __forceinline__ SmallGeo small_geo(const UniformSrc& src, uint64_t i, int g) {
     SmallGeo c;
     c.s = (int64_t)(i * src.stride);
     c.J = (src.len + (uint32_t)Geo<G>::kStep - 1u) / (uint32_t)Geo<G>::kStep;
     c.a = c.s + (int64_t)src.len - (int64_t)c.J * Geo<G>::kStep + 16 * g;
     c.la0 = c.a >= c.s ? c.a : c.s;  // the straddling lane loads at s and shifts; lanes before s reload s
-    c.r0 = ~(src.seeds ? src.seeds[i] : src.seed_all);
+    if constexpr (SEEDS) c.r0 = ~src.seeds[i];
+    else c.r0 = ~src.seed_all;
     return c;
 }
 
@@ -686,34 +688,36 @@ __device__ __forceinline__ uint32_t small_fold(const uint32_t* lds, uint32_t lan
     return finish_lanes<G>(lds, c0, c1, c2, c3);
 }
 
-template <int G, int PF, bool NT>
+template <int G, int PF, bool NT, bool SEEDS>
 __device__ __forceinline__ void uniform_small_loop(const uint32_t* lds, uint32_t lanereg, int g,
                                                    const uint8_t* __restrict__ base, const UniformSrc& src, uint64_t n,
                                                    uint64_t gid, uint64_t ngroups) {
-    u32x4 W0x, Ax[PF], W0y, Ay[PF];
-    SmallGeo cx = small_geo<G>(src, gid, g), cy;
+    // three register sets rotate: an entry's blocks are requested three entries before its fold.
+    // Loads are unconditional (a group past the batch reloads entry n - 1 and stores nothing) and
+    // the exit is wave-uniform: loads under a divergent branch leave the compiler's waits
+    // uncountable, and it then drains every load in flight (vmcnt(0)) before each fold.
+    auto geo = [&](uint64_t j) { return small_geo<G, SEEDS>(src, j < n ? j : n - 1, g); };
+    u32x4 W0x, Ax[PF], W0y, Ay[PF], W0z, Az[PF];
+    SmallGeo cx = geo(gid), cy = geo(gid + ngroups), cz = geo(gid + 2 * ngroups);
     small_load<G, PF, NT>(base, cx, W0x, Ax);
-    for (uint64_t i = gid;;) {
-        // entry i in set X; entry i + ngroups (if any) loads into Y meanwhile
-        uint64_t j = i + ngroups;
-        if (j < n) {
-            cy = small_geo<G>(src, j, g);
-            small_load<G, PF, NT>(base, cy, W0y, Ay);
-        }
-        uint32_t v = small_fold<G, PF>(lds, lanereg, cx, W0x, Ax);
-        if (g == 0) src.out[i] = ~v;
-        if (j >= n) break;
-        i = j;
-        j = i + ngroups;
-        if (j < n) {
-            cx = small_geo<G>(src, j, g);
-            small_load<G, PF, NT>(base, cx, W0x, Ax);
-        }
-        v = small_fold<G, PF>(lds, lanereg, cy, W0y, Ay);
-        if (g == 0) src.out[i] = ~v;
-        if (j >= n) break;
-        i = j;
+    small_load<G, PF, NT>(base, cy, W0y, Ay);
+    small_load<G, PF, NT>(base, cz, W0z, Az);
+    uint64_t i = gid;
+#define BKD_USMALL_STEP(C, W0C, AC)                                          \
+    {                                                                       \
+        const uint32_t v = small_fold<G, PF>(lds, lanereg, C, W0C, AC);     \
+        if (g == 0 && i < n) src.out[i] = ~v;                               \
+        C = geo(i + 3 * ngroups);                                           \
+        small_load<G, PF, NT>(base, C, W0C, AC);                            \
+        i += ngroups;                                                       \
+        if (!__any(i < n)) break;                                           \
     }
+    for (;;) {
+        BKD_USMALL_STEP(cx, W0x, Ax)
+        BKD_USMALL_STEP(cy, W0y, Ay)
+        BKD_USMALL_STEP(cz, W0z, Az)
+    }
+#undef BKD_USMALL_STEP
 }
 
 // One short-class entry of a group (kind 0 folds, 1 serial bytes, 2 bounds error, else nothing).
@@ -804,7 +808,10 @@ __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __res
     const uint64_t gid = (uint64_t)blockIdx.x * (kBlock / G) + (uint64_t)(threadIdx.x / G);
     if constexpr (std::is_same<Src, UniformSrc>::value) {
         if (src.len >= 16u && src.len <= (uint32_t)Gm::kStep * (uint32_t)(PF + 1)) {
-            if (gid < n) uniform_small_loop<G, PF, NT>(lds, lanereg, g, base, src, n, gid, ngroups);
+            if (gid < n) {
+                if (src.seeds) uniform_small_loop<G, PF, NT, true>(lds, lanereg, g, base, src, n, gid, ngroups);
+                else uniform_small_loop<G, PF, NT, false>(lds, lanereg, g, base, src, n, gid, ngroups);
+            }
             return;
         }
     }
@@ -884,6 +891,66 @@ __device__ __forceinline__ void chunk_prefetch(const uint8_t* __restrict__ base,
         const int64_t addr = (uint32_t)(k + 1) < c.J ? c.a + (int64_t)(k + 1) * Geo<G>::kStep : c.la0;
         A[k] = ld16<NT>(base + addr);
     }
+}
+
+// The lane's step-0 block of chunk `c` with the bytes in front of the chunk cleared and the seed
+// image XORed in; fx = the part of the seed image that spills into step 1's dword 0.
+template <int G>
+__device__ __forceinline__ u32x4 chunk_first_block(const ChunkGeo& c, u32x4 W0, uint32_t& fx) {
+    using Gm = Geo<G>;
+    const int32_t d0 = c.d0;
+    u32x4 w;
+    if (d0 <= 0) w = W0;
+    else if (d0 < 16) w = mask_low_bytes(W0, (uint32_t)d0);
+    else w = u32x4{0u, 0u, 0u, 0u};
+    const uint32_t r0 = c.r0;
+    if (d0 > -4 && d0 < 16) {
+        // the seed image is r0 << 8*d0 across the 16-byte block: dword k = (r0:0 >> (32 + 32k - 8*d0))
+        const uint64_t R = (uint64_t)r0 << 32;
+        auto part = [&](int k) -> uint32_t {
+            const int32_t t = 32 + 32 * k - 8 * d0;
+            return (t > 0 && t < 64) ? (uint32_t)(R >> t) : 0u;
+        };
+        w.x ^= part(0);
+        w.y ^= part(1);
+        w.z ^= part(2);
+        w.w ^= part(3);
+    }
+    fx = 0u;
+    if (d0 > Gm::kStep - 4) fx = place_seed(r0, d0 - Gm::kStep);
+    return w;
+}
+
+// Raw register of a short chunk (J <= PF + 1: every block of it is in W0 and A[0..J-2]) — the
+// arithmetic of chunk_fold without any loads (short_chunks_loop issued them chunks ahead).
+template <int G, int PF>
+__device__ __forceinline__ uint32_t short_chunk_fold(const uint32_t* lds, uint32_t lanereg, const ChunkGeo& c,
+                                                     const u32x4& W0, const u32x4 (&A)[PF]) {
+    uint32_t fx;
+    const u32x4 w = chunk_first_block<G>(c, W0, fx);
+    uint32_t c0 = w.x, c1 = w.y, c2 = w.z, c3 = w.w;
+    const uint32_t rem = c.J - 1u;
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {
+        if ((uint32_t)k < rem) {
+            c0 = mul_main_add(lds, c0, lanereg, A[k].x ^ (k == 0 ? fx : 0u));
+            c1 = mul_main_add(lds, c1, lanereg, A[k].y);
+            c2 = mul_main_add(lds, c2, lanereg, A[k].z);
+            c3 = mul_main_add(lds, c3, lanereg, A[k].w);
+        }
+    }
+    if (c.pad && c.keep < 16) {  // the last step's bytes past the entry were folded last: XOR them out
+        u32x4 last = W0;
+#pragma unroll
+        for (int k = 0; k < PF; ++k)
+            if ((uint32_t)k + 1u == rem) last = A[k];
+        const u32x4 junk = c.keep <= 0 ? last : mask_low_bytes(last, (uint32_t)c.keep);
+        c0 ^= junk.x;
+        c1 ^= junk.y;
+        c2 ^= junk.z;
+        c3 ^= junk.w;
+    }
+    return finish_lanes<G>(lds, c0, c1, c2, c3);
 }
 
 // Folds chunk `c` (its W0/A already loaded) and, once its own loads are all issued, prefetches
@@ -1038,9 +1105,75 @@ __device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lan
     return finish_lanes<G>(lds, c0, c1, c2, c3);
 }
 
-// The chunk list [0, n) in grid stride (crc_plan_chunks_kernel).
+// The short tail of the chunk list, [i, n) in grid stride: chunks of at most PF + 1 steps (the list
+// is sorted by descending step count, so they come last: config 3's 1-, 2- and 3-step heads, 437 K
+// of its 1 M). A one-step chunk is folded in ~300 VALU per wave, less than a loaded memory round
+// trip, so with one chunk prefetched (chunk_fold's X/Y sets) a group waits for memory at every
+// chunk. Here three register sets rotate: a chunk's blocks are requested three chunks before its
+// fold and its descriptor three chunks before that. Every load is unconditional (a hole or a chunk
+// past the list re-reads a real chunk's blocks), so the compiler's waits can count exactly.
 template <int G, int PF, bool NT>
-__device__ __forceinline__ void plan_chunks_loop(const uint32_t* lds, uint32_t lanereg, int g,
+__device__ __forceinline__ void short_chunks_loop(const uint32_t* lds, uint32_t lanereg, int g,
+                                                  const uint8_t* __restrict__ base, const PlanDesc* __restrict__ descs,
+                                                  uint64_t i, uint64_t n, uint64_t ngroups, uint32_t* __restrict__ out,
+                                                  uint32_t* __restrict__ partials) {
+    auto clampi = [&](uint64_t j) { return j < n ? j : n - 1; };
+    auto geo_at = [&](uint64_t j) {
+        ChunkGeo c = chunk_geo<G>(descs[clampi(j)], g);
+        if (j >= n) c.len = 0;
+        return c;
+    };
+    // blocks a hole (or a chunk past the list) loads instead: the last real chunk's, base[0, 16)
+    // before one is seen. Selected field by field: a reference to one of two geometries would put
+    // both in scratch memory.
+    int64_t fa = 0, fla0 = 0;
+    uint32_t fJ = 1u;
+    auto load = [&](const ChunkGeo& c, u32x4& W0, u32x4 (&A)[PF]) {
+        if (c.len) {
+            fa = c.a;
+            fla0 = c.la0;
+            fJ = c.J;
+        }
+        ChunkGeo t;
+        t.a = fa;
+        t.la0 = fla0;
+        t.J = fJ;
+        chunk_prefetch<G, PF, NT>(base, t, W0, A);
+    };
+    u32x4 W0x, Ax[PF], W0y, Ay[PF], W0z, Az[PF];
+    ChunkGeo cx = geo_at(i), cy = geo_at(i + ngroups), cz = geo_at(i + 2 * ngroups);
+    load(cx, W0x, Ax);
+    load(cy, W0y, Ay);
+    load(cz, W0z, Az);
+    PlanDesc dx = descs[clampi(i + 3 * ngroups)], dy = descs[clampi(i + 4 * ngroups)],
+             dz = descs[clampi(i + 5 * ngroups)];
+#define BKD_SHORT_STEP(C, W0C, AC, DC)                                                       \
+    {                                                                                        \
+        const uint32_t v = C.len ? short_chunk_fold<G, PF>(lds, lanereg, C, W0C, AC) : 0u;   \
+        if (g == 0 && C.len) {                                                               \
+            if (C.dst & kPlanFinal) out[C.dst & ~kPlanFinal] = ~v;                           \
+            else partials[C.dst] = v;                                                        \
+        }                                                                                    \
+        C = chunk_geo<G>(DC, g); /* chunk i + 3 ngroups */                                   \
+        if (i + 3 * ngroups >= n) C.len = 0;                                                 \
+        load(C, W0C, AC);                                                                    \
+        DC = descs[clampi(i + 6 * ngroups)];                                                 \
+        i += ngroups;                                                                        \
+        /* wave-uniform exit (a group past the list folds holes until its wave is done):    \
+           loads under a divergent branch would leave the compiler's waits uncountable */   \
+        if (!__any(i < n)) break;                                                            \
+    }
+    for (;;) {
+        BKD_SHORT_STEP(cx, W0x, Ax, dx)
+        BKD_SHORT_STEP(cy, W0y, Ay, dy)
+        BKD_SHORT_STEP(cz, W0z, Az, dz)
+    }
+#undef BKD_SHORT_STEP
+}
+
+// Chunks [0, n) of the list in grid stride, one prefetched chunk per group (X/Y sets).
+template <int G, int PF, bool NT>
+__device__ __forceinline__ void long_chunks_loop(const uint32_t* lds, uint32_t lanereg, int g,
                                                  const uint8_t* __restrict__ base, const PlanDesc* __restrict__ descs,
                                                  uint64_t n, uint64_t gid, uint64_t ngroups, uint32_t* __restrict__ out,
                                                  uint32_t* __restrict__ partials) {
@@ -1101,6 +1234,25 @@ __device__ __forceinline__ void plan_chunks_loop(const uint32_t* lds, uint32_t l
 #undef BKD_CHUNK_HALF
 }
 
+// Blocks per chunk in the short tail's register sets beside step 0: chunks of <= kShortPF + 1 steps
+// (PlanGeo::jshort) take short_chunks_loop.
+#ifndef BKD_SHORT_PF
+#define BKD_SHORT_PF 3
+#endif
+constexpr int kShortPF = BKD_SHORT_PF;
+
+// The chunk list [0, n) (crc_plan_chunks_kernel): [0, nmain) by long_chunks_loop, then the short
+// tail [nmain, n) by short_chunks_loop (nmain == n: no short tail).
+template <int G, int PF, bool NT>
+__device__ __forceinline__ void plan_chunks_loop(const uint32_t* lds, uint32_t lanereg, int g,
+                                                 const uint8_t* __restrict__ base, const PlanDesc* __restrict__ descs,
+                                                 uint64_t n, uint64_t nmain, uint64_t gid, uint64_t ngroups,
+                                                 uint32_t* __restrict__ out, uint32_t* __restrict__ partials) {
+    if (gid < nmain) long_chunks_loop<G, PF, NT>(lds, lanereg, g, base, descs, nmain, gid, ngroups, out, partials);
+    if (nmain < n && gid < n - nmain)
+        short_chunks_loop<G, kShortPF, NT>(lds, lanereg, g, base, descs, nmain + gid, n, ngroups, out, partials);
+}
+
 
 // Chunk kernel of the ragged-batch plan: one chunk per group, grid stride over the descriptor
 // list (sorted by step count, plan_kernels.hpp). Descriptors are read two rounds ahead and each
@@ -1130,7 +1282,9 @@ __global__ void __launch_bounds__(kBlock) crc_plan_chunks_kernel(const uint8_t* 
     const uint32_t lanereg = ((uint32_t)(lane & 31) << 2) | (1u << 16);
     const uint64_t ngroups = (uint64_t)gridDim.x * (kBlock / G);
     const uint64_t gid = (uint64_t)blockIdx.x * (kBlock / G) + (uint64_t)(threadIdx.x / G);
-    if (gid < n) plan_chunks_loop<G, PF, NT>(lds, lanereg, g, base, descs, n, gid, ngroups, out, partials);
+    // count[1]: the list position of the first chunk of at most PF + 1 steps (plan_emit_kernel)
+    const uint64_t nmain = n ? std::min<uint64_t>(n, count[1]) : 0u;
+    if (gid < n) plan_chunks_loop<G, PF, NT>(lds, lanereg, g, base, descs, n, nmain, gid, ngroups, out, partials);
     if (nov) groups_loop<G, PF, NT>(lds, lanereg, g, base, ov, nov, gid, ngroups, err);
 }
 

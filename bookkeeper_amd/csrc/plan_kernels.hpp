@@ -48,6 +48,7 @@ struct PlanGeo {
     uint32_t ch_sh;    // log2(ch) when ch is a power of two, else 0xFF (64-bit divisions are slow)
     uint32_t small;    // entries of <= small bytes belong to the short-entry launch (0: none do)
     uint32_t serial;   // entries shorter than this (16 .. kSerialMax) are computed by plan_combine
+    uint32_t jshort;   // chunks of <= jshort steps form the chunk kernel's short tail (PF + 1; 0: none)
 };
 
 // Longest entry plan_combine computes itself, one thread per entry (serial_crc).
@@ -56,6 +57,8 @@ constexpr uint32_t kSerialMax = 64u;
 // hdr words
 constexpr int kHdrTotal = 0;  // all chunks
 constexpr int kHdrWork = 2;   // descriptors to process = min(total, capacity)
+constexpr int kHdrShort = 3;  // list position of the first chunk of <= PlanGeo::jshort steps (the chunk
+                              // kernel's short tail; = total when jshort == 0)
 constexpr int kHdrBase = 4;   // kHdrBase + col: total of column col (plan_scan)
 constexpr int kHdrWords = kHdrBase + kMaxJC + 2;
 
@@ -314,6 +317,8 @@ __global__ void __launch_bounds__(kPlanBlock, BKD_PLAN_OCC) plan_emit_kernel(con
         if (blockIdx.x == 0) {  // the block that plans entry block 0, replica 0
             hdr[kHdrTotal] = acc;
             hdr[kHdrWork] = (uint32_t)((uint64_t)acc < capacity ? acc : capacity);
+            // bins of <= jshort steps come last: the short tail starts at bin jshort's first position
+            hdr[kHdrShort] = pg.jshort == 0u ? acc : (pg.jshort < pg.nbins ? bin0[pg.jshort] : 0u);
         }
     }
     __syncthreads();
