@@ -580,23 +580,26 @@ __device__ __forceinline__ SmallGeo small_geo(const UniformSrc& src, uint64_t i,
     return c;
 }
 
-// One entry's index words, loaded a round before its data (no dependent index -> data chain).
+// One entry's index words, loaded three entries before its data (no dependent index -> data
+// chain). Every load is unconditional: an index past the batch rereads entry n - 1's words and is
+// marked past; SEEDS (per-entry seeds) is a template choice, not a branch around a load.
 struct SmallIdx {
     uint64_t o;
     uint32_t l;
     uint32_t seed;
 };
 
+template <bool SEEDS>
 __device__ __forceinline__ SmallIdx small_idx(const SmallIndexedSrc& src, uint64_t i) {
+    const uint64_t j = i < src.n ? i : src.n - 1u;
     SmallIdx x;
-    if (i < src.n) {
-        x.o = src.offsets[i];
-        x.l = src.lengths[i];
-        x.seed = src.seeds ? src.seeds[i] : src.seed_all;
-    } else {
+    x.o = src.offsets[j];
+    x.l = src.lengths[j];
+    if constexpr (SEEDS) x.seed = src.seeds[j];
+    else x.seed = src.seed_all;
+    if (i >= src.n) {
         x.o = ~0ull;  // past the batch
         x.l = 0xFFFFFFFFu;
-        x.seed = 0u;
     }
     return x;
 }
@@ -617,9 +620,11 @@ __device__ __forceinline__ SmallGeo small_geo(const SmallIndexedSrc& src, const 
             c.kind = 2;
         } else {
             c.r0 = ~x.seed;
-            if (c.len < 16u) {
+            if (c.len < 16u) {  // folded serially from its one or two 16-byte blocks (la0, then a)
                 c.kind = 1;
                 c.s = (int64_t)o;
+                c.la0 = c.s & ~(int64_t)15;
+                c.a = (c.s & 15) + (int64_t)c.len > 16 ? c.la0 + 16 : 0;
             } else {
                 c.kind = 0;
                 c.s = (int64_t)o;
@@ -643,16 +648,20 @@ __device__ __forceinline__ void small_load(const uint8_t* __restrict__ base, con
     }
 }
 
-// small_load for the indexed class: only the entry's own steps (J of them) and nothing for entries
-// not folded here — no duplicate requests for 1-step entries, none for skipped ones.
+// small_load for the indexed class: every load is issued, so the compiler can count them, and a
+// block the entry does not need (steps past J, entries of other kinds) reads base[0, 16) — the same
+// line for every such lane of a wave, one request.
 template <int G, int PF, bool NT>
-__device__ __forceinline__ void small_load_exact(const uint8_t* __restrict__ base, const SmallGeo& c, u32x4& W0,
-                                                 u32x4 (&A)[PF]) {
-    if (c.kind != 0) return;
-    W0 = ld16<NT>(base + c.la0);
+__device__ __forceinline__ void small_load_idx(const uint8_t* __restrict__ base, const SmallGeo& c, u32x4& W0,
+                                               u32x4 (&A)[PF]) {
+    W0 = ld16<NT>(base + (c.kind <= 1 ? c.la0 : 0));
 #pragma unroll
-    for (int k = 0; k < PF; ++k)
-        if ((uint32_t)(k + 1) < c.J) A[k] = ld16<NT>(base + c.a + (int64_t)(k + 1) * Geo<G>::kStep);
+    for (int k = 0; k < PF; ++k) {
+        int64_t addr = 0;
+        if (c.kind == 0 && (uint32_t)(k + 1) < c.J) addr = c.a + (int64_t)(k + 1) * Geo<G>::kStep;
+        else if (c.kind == 1 && k == 0) addr = c.a;  // the second block of an entry < 16 B, or base[0, 16)
+        A[k] = ld16<NT>(base + addr);
+    }
 }
 
 // Raw register of a short entry from its loaded blocks (fold_range's arithmetic, J <= PF + 1).
@@ -720,22 +729,30 @@ __device__ __forceinline__ void uniform_small_loop(const uint32_t* lds, uint32_t
 #undef BKD_USMALL_STEP
 }
 
+// Byte p (0..15) of a 16-byte little-endian block.
+__device__ __forceinline__ uint32_t block_byte(const u32x4& v, uint32_t p) {
+    const uint32_t d = p < 4u ? v.x : p < 8u ? v.y : p < 12u ? v.z : v.w;
+    return (d >> (8u * (p & 3u))) & 0xffu;
+}
+
 // One short-class entry of a group (kind 0 folds, 1 serial bytes, 2 bounds error, else nothing).
 template <int G, int PF>
 __device__ __forceinline__ void small_entry_finish(const uint32_t* lds, uint32_t lanereg, int g,
-                                                   const uint8_t* __restrict__ base, const SmallIndexedSrc& src,
-                                                   const SmallGeo& c, uint64_t i, const u32x4& W0,
-                                                   const u32x4 (&A)[PF], uint32_t* __restrict__ err) {
+                                                   const SmallIndexedSrc& src, const SmallGeo& c, uint64_t i,
+                                                   const u32x4& W0, const u32x4 (&A)[PF], uint32_t* __restrict__ err) {
     using Gm = Geo<G>;
     if (c.kind == 0) {
         const uint32_t v = small_fold<G, PF>(lds, lanereg, c, W0, A);
         if (g == 0) src.out[i] = ~v;
-    } else if (c.kind == 1) {  // < 16 B: serial byte loop (ReflectedIntCrc.java:44-48 form)
+    } else if (c.kind == 1) {  // < 16 B: byte-at-a-time from its loaded blocks (ReflectedIntCrc.java:44-48 form)
         if (g == 0) {
             uint32_t r = c.r0;
-            const uint8_t* q = base + c.s;
-            for (uint32_t k = 0; k < c.len; ++k)
-                r = lds_word(lds, Gm::kByteTabOff + (((r ^ q[k]) & 0xffu) << 2)) ^ (r >> 8);
+            const uint32_t off = (uint32_t)(c.s & 15);
+            for (uint32_t k = 0; k < c.len; ++k) {
+                const uint32_t p = off + k;
+                const uint32_t b = p < 16u ? block_byte(W0, p) : block_byte(A[0], p - 16u);
+                r = lds_word(lds, Gm::kByteTabOff + (((r ^ b) & 0xffu) << 2)) ^ (r >> 8);
+            }
             src.out[i] = ~r;
         }
     } else if (c.kind == 2) {
@@ -746,47 +763,44 @@ __device__ __forceinline__ void small_entry_finish(const uint32_t* lds, uint32_t
     }
 }
 
-// The short-entry class of an indexed batch (SmallIndexedSrc), with uniform_small_loop's X/Y
-// lookahead: a group's next entry is loaded while the current one folds. Entries of other kinds
-// take their branch (serial bytes, bounds error, skip) without loads of their own.
+// The short-entry class of an indexed batch (SmallIndexedSrc). Three register sets rotate, as in
+// uniform_small_loop: an entry's blocks are requested three entries before it is folded and its
+// index words three entries before that. Every load is unconditional and the exit wave-uniform
+// (a group past the batch walks "past" entries until its wave is done), so the compiler's waits
+// count the loads in flight instead of draining them at every entry.
 // Returns whether this lane met an entry of the plan's (kind 3).
-template <int G, int PF, bool NT>
+template <int G, int PF, bool NT, bool SEEDS>
 __device__ __forceinline__ bool indexed_small_loop(const uint32_t* lds, uint32_t lanereg, int g,
                                                    const uint8_t* __restrict__ base, const SmallIndexedSrc& src,
                                                    uint64_t n, uint64_t gid, uint64_t ngroups,
                                                    uint32_t* __restrict__ err) {
     bool saw_plan = false;
-    auto finish = [&](const SmallGeo& c, uint64_t i, const u32x4& W0, const u32x4(&A)[PF]) {
-        saw_plan |= c.kind == 3;
-        small_entry_finish<G, PF>(lds, lanereg, g, base, src, c, i, W0, A, err);
-    };
-    // index words two entries ahead, data one entry ahead (X/Y register sets)
-    u32x4 W0x, Ax[PF], W0y, Ay[PF];
-    SmallGeo cx = small_geo<G>(src, small_idx(src, gid), g), cy;
-    SmallIdx nx = small_idx(src, gid + ngroups);
-    small_load_exact<G, PF, NT>(base, cx, W0x, Ax);
-    for (uint64_t i = gid;;) {
-        uint64_t j = i + ngroups;
-        SmallIdx nn = small_idx(src, j + ngroups);
-        if (j < n) {
-            cy = small_geo<G>(src, nx, g);
-            small_load_exact<G, PF, NT>(base, cy, W0y, Ay);
-        }
-        finish(cx, i, W0x, Ax);
-        if (j >= n) break;
-        i = j;
-        nx = nn;
-        j = i + ngroups;
-        nn = small_idx(src, j + ngroups);
-        if (j < n) {
-            cx = small_geo<G>(src, nx, g);
-            small_load_exact<G, PF, NT>(base, cx, W0x, Ax);
-        }
-        finish(cy, i, W0y, Ay);
-        if (j >= n) break;
-        i = j;
-        nx = nn;
+    auto geo = [&](const SmallIdx& x) { return small_geo<G>(src, x, g); };
+    u32x4 W0x, Ax[PF], W0y, Ay[PF], W0z, Az[PF];
+    SmallGeo cx = geo(small_idx<SEEDS>(src, gid)), cy = geo(small_idx<SEEDS>(src, gid + ngroups)),
+             cz = geo(small_idx<SEEDS>(src, gid + 2 * ngroups));
+    small_load_idx<G, PF, NT>(base, cx, W0x, Ax);
+    small_load_idx<G, PF, NT>(base, cy, W0y, Ay);
+    small_load_idx<G, PF, NT>(base, cz, W0z, Az);
+    SmallIdx ix = small_idx<SEEDS>(src, gid + 3 * ngroups), iy = small_idx<SEEDS>(src, gid + 4 * ngroups),
+             iz = small_idx<SEEDS>(src, gid + 5 * ngroups);
+    uint64_t i = gid;
+#define BKD_ISMALL_STEP(C, W0C, AC, IC)                                                \
+    {                                                                                 \
+        saw_plan |= C.kind == 3;                                                      \
+        small_entry_finish<G, PF>(lds, lanereg, g, src, C, i, W0C, AC, err);          \
+        C = geo(IC); /* entry i + 3 ngroups */                                        \
+        small_load_idx<G, PF, NT>(base, C, W0C, AC);                                  \
+        IC = small_idx<SEEDS>(src, i + 6 * ngroups);                                  \
+        i += ngroups;                                                                 \
+        if (!__any(i < n)) break;                                                     \
     }
+    for (;;) {
+        BKD_ISMALL_STEP(cx, W0x, Ax, ix)
+        BKD_ISMALL_STEP(cy, W0y, Ay, iy)
+        BKD_ISMALL_STEP(cz, W0z, Az, iz)
+    }
+#undef BKD_ISMALL_STEP
     return saw_plan;
 }
 
@@ -817,7 +831,10 @@ __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __res
     }
     if constexpr (std::is_same<Src, SmallIndexedSrc>::value) {
         bool saw = false;
-        if (gid < n) saw = indexed_small_loop<G, PF, NT>(lds, lanereg, g, base, src, n, gid, ngroups, err);
+        if (gid < n) {
+            if (src.seeds) saw = indexed_small_loop<G, PF, NT, true>(lds, lanereg, g, base, src, n, gid, ngroups, err);
+            else saw = indexed_small_loop<G, PF, NT, false>(lds, lanereg, g, base, src, n, gid, ngroups, err);
+        }
         if (__any(saw) && (threadIdx.x & 63) == 0 && src.plan_flag) *src.plan_flag = src.plan_epoch;
     } else {
         groups_loop<G, PF, NT>(lds, lanereg, g, base, src, n, gid, ngroups, err);
