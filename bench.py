@@ -474,7 +474,8 @@ def digest_bench(args, ck, torch, rank, dev, stream, algo) -> None:
            "all_verified": ok,
            "roofline": {"bound": "hbm", "achieved": round(v_bytes / t_verify / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(v_bytes / t_verify / 1e9 / HBM_PEAK_GBS, 4),
-                        "traffic": None, "kernel": "verify pipeline (length gate + fused verify kernel for near-uniform frames; header + plan + finish otherwise)",
+                        "traffic": _pmc_traffic("verify4k" if algo == ck.CRC32C else "verify4k_crc32"),
+                        "kernel": "verify pipeline (length gate + fused verify kernel for near-uniform frames; header + plan + finish otherwise)",
                         "algorithmic_bytes_per_launch": v_bytes},
            "package": {"GiB_s_payload": round(n * plen / t_pack / GIB, 2), "ms": round(t_pack * 1e3, 4),
                        "achieved_GB_s": round(p_bytes / t_pack / 1e9, 1),
