@@ -1259,6 +1259,10 @@ int bkd_crc_batch_uniform(int algo, const void* d_base, uint64_t stride, uint32_
     int lanes = auto_lanes(entry_len, n, ds->cus);
     if (g_forced_lanes.load() == 0 && entry_len >= 16u && entry_len <= 48u && n >= (uint64_t)ds->cus * bkd::kBlock)
         lanes = 1;
+    // 256..511 B: 8 lanes (two to four 128-byte steps; the three-set short loop up to 384 B) beat 4
+    // lanes since the short loop's waits are countable: 256 B 0.934 vs 1.028 ms, 512 B 0.826 vs
+    // 0.915 ms per 4 GiB (profiles/r03v_size_sweep.log); indexed batches keep auto_lanes
+    if (g_forced_lanes.load() == 0 && lanes == 4 && entry_len >= 256u && entry_len < 512u) lanes = 8;
     if (lanes == 8 && entry_len >= bkd::kTailUncondSteps * 16u * 8u)  // measured at 8 lanes only
         return dispatch_lanes(*ds, lanes, algo, (const uint8_t*)d_base, bkd::UniformLongSrc{src}, n, st);
     return dispatch_lanes(*ds, lanes, algo, (const uint8_t*)d_base, src, n, st);

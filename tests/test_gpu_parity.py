@@ -167,6 +167,27 @@ def test_uniform_short_entries_seeded(gpu, lanes):
         assert (got.cpu().numpy().view(np.uint32) == want).all(), (entry_len, stride, n)
 
 
+def test_uniform_auto_lanes_short_entries(gpu):
+    """Automatic lane choice across the short-entry sizes (1 lane to 48 B, 4 lanes to 255 B, 8 lanes
+    from 256 B), seeded and unseeded, batches smaller and larger than the grid."""
+    import torch
+    ck.set_group_lanes(0)
+    rng = np.random.default_rng(7)
+    for entry_len, stride, n in [(200, 200, 5000), (255, 257, 3001), (256, 256, 300000), (300, 301, 70001),
+                                 (384, 384, 40000), (385, 390, 9999), (511, 512, 20000)]:
+        nbytes = (n - 1) * stride + entry_len
+        data = oracle.fill_splitmix64(nbytes, entry_len)
+        base = _dev_bytes(torch, data, gpu)
+        offs = np.arange(n, dtype=np.uint64) * stride
+        lens = np.full(n, entry_len, dtype=np.uint32)
+        seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        got = ck.crc_batch_uniform(ck.CRC32C, base, entry_len, n, stride=stride,
+                                   seeds=torch.from_numpy(seeds.view(np.int32)).to(gpu))
+        assert (got.cpu().numpy().view(np.uint32) == oracle.batch(ck.CRC32C, data, offs, lens, seeds=seeds)).all()
+        got = ck.crc_batch_uniform(ck.CRC32, base, entry_len, n, stride=stride, seed_all=0x1234)
+        assert (got.cpu().numpy().view(np.uint32) == oracle.uniform(ck.CRC32, data, stride, entry_len, n, 0x1234)).all()
+
+
 def test_uniform_tiny_entries_auto_one_lane(gpu):
     """16..48-byte uniform entries in large batches pick one lane per entry automatically."""
     import torch
