@@ -99,6 +99,47 @@ __device__ __forceinline__ uint32_t mul_main_add(const uint32_t* lds, uint32_t v
 #endif
 }
 
+#ifndef BKD_CLOCK_ADAPT
+#define BKD_CLOCK_ADAPT 1  // 0: the one-entry-per-group fold always uses mul_main_add
+#endif
+#ifndef BKD_LOW_CLOCK_MHZ
+#define BKD_LOW_CLOCK_MHZ 2000
+#endif
+constexpr uint64_t kLowClockMHz = BKD_LOW_CLOCK_MHZ;
+
+// One fold step of the four dword streams, c_k = c_k * C_main ^ d_k, with all 16 table lookups in
+// flight at once and the XORs as v_bitop3: the compiler's schedule (mul_main_add) issues them 8 at
+// a time and drains (lgkmcnt(0)) between the batches, two LDS round trips per step. Faster when the
+// shader clock is power-limited, slower at full clock: groups_loop picks one per
+// launch from the clock it measures (crc_groups_kernel). The lookups are inline-asm ds_read_b32 from
+// the kernel's LDS image (its only __shared__ array, at LDS address 0: the byte addresses v_perm
+// builds are absolute), followed by one s_waitcnt that takes every result as an operand, so no use
+// can be scheduled before it.
+__device__ __forceinline__ void fold4_main(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t lanereg,
+                                           uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3) {
+    uint32_t t[16];
+    const uint32_t cs[4] = {c0, c1, c2, c3};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t a0 = __builtin_amdgcn_perm(cs[k], lanereg, 0x0C0C0400u);
+        const uint32_t a1 = __builtin_amdgcn_perm(cs[k], lanereg, 0x0C0C0500u);
+        const uint32_t a2 = __builtin_amdgcn_perm(cs[k], lanereg, 0x0C020600u);
+        const uint32_t a3 = __builtin_amdgcn_perm(cs[k], lanereg, 0x0C020700u);
+        asm volatile("ds_read_b32 %0, %1" : "=v"(t[4 * k + 0]) : "v"(a0));
+        asm volatile("ds_read_b32 %0, %1 offset:128" : "=v"(t[4 * k + 1]) : "v"(a1));
+        asm volatile("ds_read_b32 %0, %1" : "=v"(t[4 * k + 2]) : "v"(a2));
+        asm volatile("ds_read_b32 %0, %1 offset:128" : "=v"(t[4 * k + 3]) : "v"(a3));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]), "+v"(t[7]),
+                   "+v"(t[8]), "+v"(t[9]), "+v"(t[10]), "+v"(t[11]), "+v"(t[12]), "+v"(t[13]), "+v"(t[14]),
+                   "+v"(t[15]));
+    c0 = xor3(xor3(t[0], t[1], t[2]), t[3], d0);
+    c1 = xor3(xor3(t[4], t[5], t[6]), t[7], d1);
+    c2 = xor3(xor3(t[8], t[9], t[10]), t[11], d2);
+    c3 = xor3(xor3(t[12], t[13], t[14]), t[15], d3);
+}
+
 __device__ __forceinline__ uint32_t mul_main(const uint32_t* lds, uint32_t v, uint32_t lanereg) {
     return mul_main_add(lds, v, lanereg, 0u);
 }
@@ -409,7 +450,8 @@ __device__ __forceinline__ void stage_tables(uint32_t* lds, const uint32_t* __re
 // profiles/r03f_ab_variants_order*.log); indexed and framed batches did not gain (package +1.5 %),
 // and short uniform entries lost (512 B +13 %, 1 KiB +2.7 %: most of their loads are tail loads,
 // profiles/r03g_ab_order*.log)
-template <int G, int PF, bool NT, bool ALIGNED, bool TAILU = BKD_TAIL_UNCOND != 0>
+// B16: each fold step through fold4_main (16 lookups in flight) instead of mul_main_add.
+template <int G, int PF, bool NT, bool ALIGNED, bool TAILU = BKD_TAIL_UNCOND != 0, bool B16 = false>
 __device__ __forceinline__ uint32_t fold_range(const uint32_t* lds, uint32_t lanereg, int g,
                                                const uint8_t* __restrict__ base, int64_t s, int64_t e, uint32_t r0) {
     using Gm = Geo<G>;
@@ -443,20 +485,28 @@ __device__ __forceinline__ uint32_t fold_range(const uint32_t* lds, uint32_t lan
     // unconditionally (a conditional load would merge registers and force an early vmcnt(0)).
     const uint8_t* p = base + a + Gm::kStep;
     const uint32_t rem = J - 1u;
-#define BKD_FOLD0(d)                                     \
-    do {                                                 \
-        c0 = mul_main_add(lds, c0, lanereg, (d).x ^ fx);    \
-        fx = 0u;                                         \
-        c1 = mul_main_add(lds, c1, lanereg, (d).y);         \
-        c2 = mul_main_add(lds, c2, lanereg, (d).z);         \
-        c3 = mul_main_add(lds, c3, lanereg, (d).w);         \
+#define BKD_FOLD0(d)                                                                  \
+    do {                                                                              \
+        if constexpr (B16) {                                                          \
+            fold4_main(c0, c1, c2, c3, lanereg, (d).x ^ fx, (d).y, (d).z, (d).w);     \
+        } else {                                                                      \
+            c0 = mul_main_add(lds, c0, lanereg, (d).x ^ fx);                          \
+            c1 = mul_main_add(lds, c1, lanereg, (d).y);                               \
+            c2 = mul_main_add(lds, c2, lanereg, (d).z);                               \
+            c3 = mul_main_add(lds, c3, lanereg, (d).w);                               \
+        }                                                                             \
+        fx = 0u;                                                                      \
     } while (0)
-#define BKD_FOLD(d)                                  \
-    do {                                             \
-        c0 = mul_main_add(lds, c0, lanereg, (d).x);     \
-        c1 = mul_main_add(lds, c1, lanereg, (d).y);     \
-        c2 = mul_main_add(lds, c2, lanereg, (d).z);     \
-        c3 = mul_main_add(lds, c3, lanereg, (d).w);     \
+#define BKD_FOLD(d)                                                                   \
+    do {                                                                              \
+        if constexpr (B16) {                                                          \
+            fold4_main(c0, c1, c2, c3, lanereg, (d).x, (d).y, (d).z, (d).w);          \
+        } else {                                                                      \
+            c0 = mul_main_add(lds, c0, lanereg, (d).x);                               \
+            c1 = mul_main_add(lds, c1, lanereg, (d).y);                               \
+            c2 = mul_main_add(lds, c2, lanereg, (d).z);                               \
+            c3 = mul_main_add(lds, c3, lanereg, (d).w);                               \
+        }                                                                             \
     } while (0)
     if (rem >= (uint32_t)PF) {
         // A/B register double buffer: fold one block while the other block's loads fly.
@@ -523,10 +573,12 @@ __device__ __forceinline__ uint32_t fold_range(const uint32_t* lds, uint32_t lan
 }
 
 // Grid-stride loop of the one-entry-per-group kernels: work items gid, gid + ngroups, ... of `src`.
+// low_clock: fold each entry through fold4_main (crc_groups_kernel measured a power-limited clock).
 template <int G, int PF, bool NT, class Src>
 __device__ __forceinline__ void groups_loop(const uint32_t* lds, uint32_t lanereg, int g,
                                             const uint8_t* __restrict__ base, const Src& src, uint64_t n,
-                                            uint64_t gid, uint64_t ngroups, uint32_t* __restrict__ err) {
+                                            uint64_t gid, uint64_t ngroups, uint32_t* __restrict__ err,
+                                            bool low_clock = false) {
     using Gm = Geo<G>;
     for (uint64_t i = gid; i < n; i += ngroups) {
         Work wk;
@@ -548,9 +600,10 @@ __device__ __forceinline__ void groups_loop(const uint32_t* lds, uint32_t lanere
             }
             continue;
         }
+        constexpr bool kTailU = BKD_TAIL_UNCOND != 0 || std::is_same<Src, UniformLongSrc>::value;
         const uint32_t v =
-            fold_range<G, PF, NT, false, BKD_TAIL_UNCOND != 0 || std::is_same<Src, UniformLongSrc>::value>(
-                lds, lanereg, g, base, wk.s, wk.s + (int64_t)wk.len, wk.r0);
+            low_clock ? fold_range<G, PF, NT, false, kTailU, true>(lds, lanereg, g, base, wk.s, wk.s + (int64_t)wk.len, wk.r0)
+                      : fold_range<G, PF, NT, false, kTailU, false>(lds, lanereg, g, base, wk.s, wk.s + (int64_t)wk.len, wk.r0);
         if (g == 0) put_result(src, i, wk, v ^ wk.xorout);
     }
 }
@@ -813,7 +866,12 @@ __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __res
     __shared__ __attribute__((aligned(16))) uint32_t lds[Gm::kLdsWords];
     const uint64_t n = src.count();
     if (n == 0) return;
+    // the shader clock over the table staging (shader cycles against the 100 MHz real-time counter,
+    // both scalar reads): below kLowClockMHz the one-entry-per-group fold takes fold4_main
+    const uint64_t clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
     stage_tables<G>(lds, tables);
+    const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+    const bool low_clock = BKD_CLOCK_ADAPT && (clk1 - clk0) * 100u < (rt1 - rt0) * (uint64_t)kLowClockMHz;
 
     const int lane = threadIdx.x & 63;
     const int g = lane & (G - 1);
@@ -837,7 +895,7 @@ __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __res
         }
         if (__any(saw) && (threadIdx.x & 63) == 0 && src.plan_flag) *src.plan_flag = src.plan_epoch;
     } else {
-        groups_loop<G, PF, NT>(lds, lanereg, g, base, src, n, gid, ngroups, err);
+        groups_loop<G, PF, NT>(lds, lanereg, g, base, src, n, gid, ngroups, err, low_clock);
     }
 }
 
