@@ -378,6 +378,11 @@ def set_group_lanes(lanes: int) -> None:
     check(lib().bkd_set_group_lanes(lanes))
 
 
+def set_fold_schedule(schedule: int) -> None:
+    """0 = by the measured shader clock (default), 1 = compiler schedule, 2 = low-clock schedule."""
+    check(lib().bkd_set_fold_schedule(schedule))
+
+
 def set_plan_mode(mode: int) -> None:
     """0 = auto, 1 = one entry per lane group, 2 = chunked plan (indexed batches)."""
     check(lib().bkd_set_plan_mode(mode))

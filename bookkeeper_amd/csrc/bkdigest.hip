@@ -184,6 +184,7 @@ std::atomic<int> g_plan_mode{0};  // 0 auto, 1 direct (one entry per group), 2 c
 std::atomic<int> g_plan_lanes{8};
 std::atomic<int> g_plan_jc{32};
 std::atomic<int> g_plan_merge{16};
+std::atomic<int> g_fold_sched{0};  // bkd_set_fold_schedule: 0 by the measured clock, 1 fixed, 2 low-clock
 std::atomic<int> g_plan_pf{2};  // loads in flight per lane in the chunk kernel (2, 4 or 8)
 // Short-entry class of indexed batches: entries of <= this many bytes skip the plan and run in
 // their own launch (4-lane groups, next entry loaded during the current one). 0 = none.
@@ -368,7 +369,7 @@ int launch_groups(DeviceState& ds, int algo, const uint8_t* base, const Src& src
     blocks = std::min<uint64_t>(blocks, (uint64_t)ds.cus);
     const uint32_t* tab = ds.tables[algo][lane_index(G)];
     hipLaunchKernelGGL((bkd::crc_groups_kernel<G, kPF, kNT, Src>), dim3((unsigned)blocks), dim3(bkd::kBlock), 0,
-                       stream, base, src, tab, err);
+                       stream, base, src, tab, err, g_fold_sched.load());
     BKD_HIP(hipGetLastError());
     return BKD_OK;
 }
@@ -484,7 +485,7 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
         const uint64_t per_block = bkd::kBlock / kSmallLanes;
         const unsigned sblocks = (unsigned)std::min<uint64_t>((n + per_block - 1) / per_block, (uint64_t)ds.cus);
         hipLaunchKernelGGL((bkd::crc_groups_kernel<kSmallLanes, 2, kNT, bkd::SmallIndexedSrc>), dim3(sblocks),
-                           dim3(bkd::kBlock), 0, st, base, ss, ds.tables[algo][lane_index(kSmallLanes)], err);
+                           dim3(bkd::kBlock), 0, st, base, ss, ds.tables[algo][lane_index(kSmallLanes)], err, 1);
     }
     // count / emit / combine walk their 1024-entry blocks in grid stride (BKD_PLAN_GRID blocks per CU;
     // 0: one block per entry block)
@@ -1190,6 +1191,12 @@ int bkd_init(int device) {
 }
 
 const char* bkd_last_error(void) { return t_err.c_str(); }
+
+int bkd_set_fold_schedule(int schedule) {
+    if (schedule < 0 || schedule > 2) return fail(BKD_ERR_INVALID_ARG, "fold schedule must be 0, 1 or 2");
+    g_fold_sched.store(schedule);
+    return BKD_OK;
+}
 
 int bkd_set_group_lanes(int lanes) {
     if (lanes != 0 && lane_index(lanes) < 0) return fail(BKD_ERR_INVALID_ARG, "lanes must be 0, 1, 4, 8, 16, 32 or 64");

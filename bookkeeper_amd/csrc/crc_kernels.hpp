@@ -859,9 +859,10 @@ __device__ __forceinline__ bool indexed_small_loop(const uint32_t* lds, uint32_t
 
 // One CRC per work item of `src` (uniform / indexed / framed-payload entries), persistent grid.
 template <int G, int PF, bool NT, class Src>
+// sched: 0 chosen from the measured clock, 1 mul_main_add, 2 fold4_main (bkd_set_fold_schedule)
 __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __restrict__ base, Src src,
                                                             const uint32_t* __restrict__ tables,
-                                                            uint32_t* __restrict__ err) {
+                                                            uint32_t* __restrict__ err, int sched) {
     using Gm = Geo<G>;
     __shared__ __attribute__((aligned(16))) uint32_t lds[Gm::kLdsWords];
     const uint64_t n = src.count();
@@ -871,7 +872,8 @@ __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __res
     const uint64_t clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
     stage_tables<G>(lds, tables);
     const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
-    const bool low_clock = BKD_CLOCK_ADAPT && (clk1 - clk0) * 100u < (rt1 - rt0) * (uint64_t)kLowClockMHz;
+    const bool low_clock = sched == 2 || (sched == 0 && BKD_CLOCK_ADAPT &&
+                                          (clk1 - clk0) * 100u < (rt1 - rt0) * (uint64_t)kLowClockMHz);
 
     const int lane = threadIdx.x & 63;
     const int g = lane & (G - 1);

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define BKD_ABI_VERSION 4
+#define BKD_ABI_VERSION 5
 
 /* only the entry points below are exported (the library is built with -fvisibility=hidden) */
 #ifndef BKD_API
@@ -291,6 +291,11 @@ BKD_API int bkd_set_plan_small(uint32_t max_bytes);
 BKD_API int bkd_set_plan_serial(uint32_t bytes);
 /* Register double-buffer depth of the plan's chunk kernel (2, 4 or 8 loads per lane). */
 BKD_API int bkd_set_plan_prefetch(int loads_in_flight);
+/* Fold schedule of the one-entry-per-group kernels (uniform, direct indexed, package payloads):
+ * 0 = chosen per launch from the shader clock the kernel measures (the low-clock schedule below
+ * 2 GHz), 1 = always the compiler's schedule, 2 = always the low-clock schedule
+ * (16 table lookups in flight per step). Results are identical; only the speed differs. */
+BKD_API int bkd_set_fold_schedule(int schedule);
 BKD_API int bkd_get_group_lanes(int algo, uint64_t mean_len);
 
 #ifdef __cplusplus

@@ -188,6 +188,45 @@ def test_uniform_auto_lanes_short_entries(gpu):
         assert (got.cpu().numpy().view(np.uint32) == oracle.uniform(ck.CRC32, data, stride, entry_len, n, 0x1234)).all()
 
 
+@pytest.mark.parametrize("schedule", [1, 2])
+def test_fold_schedules_bit_exact(gpu, schedule):
+    """Both fold schedules of the one-entry-per-group kernels (the compiler's and the low-clock one
+    that keeps a step's 16 lookups in flight; the default picks one from the measured clock):
+    uniform entries across lane widths with per-entry seeds, and the direct indexed kernel on
+    unaligned ragged entries (CRC32C and CRC32), against the oracle."""
+    import torch
+    ck.set_fold_schedule(schedule)
+    try:
+        rng = np.random.default_rng(schedule)
+        for lanes, entry_len, stride, n in [(8, 4096, 4096, 5000), (16, 16384, 16400, 300), (32, 70000, 70003, 40),
+                                            (4, 1000, 1003, 3000), (8, 700, 700, 9000)]:
+            ck.set_group_lanes(lanes)
+            nbytes = (n - 1) * stride + entry_len
+            data = oracle.fill_splitmix64(nbytes, entry_len + schedule)
+            base = _dev_bytes(torch, data, gpu)
+            seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+            got = ck.crc_batch_uniform(ck.CRC32C, base, entry_len, n, stride=stride,
+                                       seeds=torch.from_numpy(seeds.view(np.int32)).to(gpu))
+            offs = np.arange(n, dtype=np.uint64) * stride
+            want = oracle.batch(ck.CRC32C, data, offs, np.full(n, entry_len, dtype=np.uint32), seeds=seeds)
+            assert (got.cpu().numpy().view(np.uint32) == want).all(), (lanes, entry_len)
+        ck.set_group_lanes(0)
+        ck.set_plan_mode(1)  # the direct indexed kernel: one entry per group
+        n = 4000
+        data = oracle.fill_splitmix64(8 << 20, 99 + schedule)
+        base = _dev_bytes(torch, data, gpu)
+        lens = rng.integers(0, 9000, n).astype(np.uint32)
+        offs = rng.integers(0, (8 << 20) - 9000, n).astype(np.uint64)
+        for algo in (ck.CRC32C, ck.CRC32):
+            got = ck.crc_batch(algo, base, torch.from_numpy(offs.astype(np.int64)).to(gpu),
+                               torch.from_numpy(lens.astype(np.int32)).to(gpu))
+            assert (got.cpu().numpy().view(np.uint32) == oracle.batch(algo, data, offs, lens)).all(), algo
+    finally:
+        ck.set_fold_schedule(0)
+        ck.set_plan_mode(0)
+        ck.set_group_lanes(0)
+
+
 def test_uniform_tiny_entries_auto_one_lane(gpu):
     """16..48-byte uniform entries in large batches pick one lane per entry automatically."""
     import torch

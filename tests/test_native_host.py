@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     assert set(declared) <= exported
     # nothing but the declared entry points leaks as a C symbol (C++ kernel stubs are mangled)
     assert {x for x in exported if not x.startswith("_Z") and not x.startswith("__hip")} == set(declared)
-    assert L.bkd_abi_version() == 4  # 3: bkd_stream_release; 4: host batch routes, bkd_host_release
+    assert L.bkd_abi_version() == 5  # 3: bkd_stream_release; 4: host batch routes, bkd_host_release; 5: bkd_set_fold_schedule
 
 
 def test_library_contains_gfx950_code():
