@@ -913,7 +913,7 @@ void launch_verify_fused(DeviceState& ds, hipStream_t st, int algo, const uint8_
     const unsigned blocks = (unsigned)std::min<uint64_t>((n + per_block - 1) / per_block, (uint64_t)ds.cus);
     hipLaunchKernelGGL((bkd::crc_verify_fused_kernel<G, kPF, kNT>), dim3(blocks), dim3(bkd::kBlock), 0, st, framed, size,
                        offsets, lengths, n, mac, ledger_id, first_entry_id, id_checks, ds.tables[algo][lane_index(G)],
-                       status, (unsigned long long*)first_bad, vflag, vepoch);
+                       status, (unsigned long long*)first_bad, vflag, vepoch, g_fold_sched.load());
 }
 
 // Verify (bkd_digest_verify_batch and bkd_entrylog_verify): header CRCs -> payload CRCs seeded

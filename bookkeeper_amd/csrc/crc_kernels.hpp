@@ -1569,11 +1569,16 @@ __global__ void __launch_bounds__(kBlock) crc_verify_fused_kernel(
     const uint8_t* __restrict__ base, uint64_t size, const uint64_t* __restrict__ offsets,
     const uint32_t* __restrict__ lengths, uint64_t n, uint32_t mac, int64_t ledger_id, int64_t first_entry_id,
     int id_checks, const uint32_t* __restrict__ tables, int32_t* __restrict__ status,
-    unsigned long long* __restrict__ first_bad, const uint32_t* __restrict__ vflag, uint32_t vepoch) {
+    unsigned long long* __restrict__ first_bad, const uint32_t* __restrict__ vflag, uint32_t vepoch, int sched) {
     using Gm = Geo<G>;
     if (*vflag == vepoch) return;  // some frame out of band: the header / plan / finish sequence runs
     __shared__ __attribute__((aligned(16))) uint32_t lds[Gm::kLdsWords];
+    // payload fold schedule from the shader clock over the table staging (as crc_groups_kernel)
+    const uint64_t clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
     stage_tables<G>(lds, tables);
+    const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+    const bool low_clock = sched == 2 || (sched == 0 && BKD_CLOCK_ADAPT &&
+                                          (clk1 - clk0) * 100u < (rt1 - rt0) * (uint64_t)kLowClockMHz);
     const int lane = threadIdx.x & 63;
     const int g = lane & (G - 1);
     const uint32_t lanereg = ((uint32_t)(lane & 31) << 2) | (1u << 16);
@@ -1601,7 +1606,8 @@ __global__ void __launch_bounds__(kBlock) crc_verify_fused_kernel(
                 for (const uint8_t* q = base + s; q < base + e; ++q)
                     v = lds_word(lds, Gm::kByteTabOff + (((v ^ *q) & 0xffu) << 2)) ^ (v >> 8);
             } else {
-                v = fold_range<G, PF, NT, false>(lds, lanereg, g, base, s, e, reg);
+                v = low_clock ? fold_range<G, PF, NT, false, BKD_TAIL_UNCOND != 0, true>(lds, lanereg, g, base, s, e, reg)
+                              : fold_range<G, PF, NT, false, BKD_TAIL_UNCOND != 0, false>(lds, lanereg, g, base, s, e, reg);
             }
             const uint32_t computed = ~v;
             // digest: 4-byte BE int (CRC32C) or 8-byte BE zero-extended long (CRC32) at offset 32

@@ -192,8 +192,9 @@ def test_uniform_auto_lanes_short_entries(gpu):
 def test_fold_schedules_bit_exact(gpu, schedule):
     """Both fold schedules of the one-entry-per-group kernels (the compiler's and the low-clock one
     that keeps a step's 16 lookups in flight; the default picks one from the measured clock):
-    uniform entries across lane widths with per-entry seeds, and the direct indexed kernel on
-    unaligned ragged entries (CRC32C and CRC32), against the oracle."""
+    uniform entries across lane widths with per-entry seeds, the direct indexed kernel on unaligned
+    ragged entries (CRC32C and CRC32), DigestManager package payloads and the fused verify route,
+    against the oracle."""
     import torch
     ck.set_fold_schedule(schedule)
     try:
@@ -221,6 +222,10 @@ def test_fold_schedules_bit_exact(gpu, schedule):
             got = ck.crc_batch(algo, base, torch.from_numpy(offs.astype(np.int64)).to(gpu),
                                torch.from_numpy(lens.astype(np.int32)).to(gpu))
             assert (got.cpu().numpy().view(np.uint32) == oracle.batch(algo, data, offs, lens)).all(), algo
+        ck.set_plan_mode(0)
+        # package payloads (one entry per group) and the fused verify route under the same schedule
+        test_digest_batch_package_and_verify(gpu, dg.DigestType.CRC32C, ck.CRC32C)
+        test_verify_batch_near_uniform_frames(gpu, dg.DigestType.CRC32, ck.CRC32, False)
     finally:
         ck.set_fold_schedule(0)
         ck.set_plan_mode(0)
