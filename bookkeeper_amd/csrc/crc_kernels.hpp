@@ -385,6 +385,9 @@ __device__ __forceinline__ uint32_t finish_lanes(const uint32_t* lds, uint32_t c
         return mul_main_add(lds, c0, lanereg,
                             mul_aux_add(lds, Gm::kX96Off, c1, mul_aux_add(lds, Gm::kX64Off, c2, mul_aux(lds, Gm::kX32Off, c3))));
     } else if constexpr (Gm::kLaneTab) {
+#if BKD_FINISH_PROBE
+        return c0 ^ c1 ^ c2 ^ c3;  // measurement-only build: the finish's cost (wrong digests)
+#endif
         // one more product per lane, by its weight x^(128 (G-1-g)) in the group's register (eight
         // nibble lookups, independent), then an XOR over the group's lanes by DPP: one dependent
         // LDS round trip instead of log2(G)

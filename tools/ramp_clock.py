@@ -37,6 +37,7 @@ def main() -> None:
     ap.add_argument("--idle-ms", type=float, default=2000.0)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--probe", action="store_true")
+    ap.add_argument("--no-check", action="store_true", help="measurement-only builds whose digests differ")
     args = ap.parse_args()
     import torch
     libs = args.libs or [os.path.join(ROOT, "bookkeeper_amd", "libbkdigest.so")]
@@ -73,7 +74,7 @@ def main() -> None:
             torch.cuda.synchronize()
             if ref is None:
                 ref = out.clone()
-            assert torch.equal(out, ref), "builds disagree"
+            assert args.no_check or torch.equal(out, ref), "builds disagree"
             ms = [a.elapsed_time(b) for a, b in evs]
             res = {"lib": name, "round": rnd, "idle_ms": args.idle_ms, "probe": bool(probe),
                    "mean_5_25": round(sum(ms[5:25]) / 20, 4),
