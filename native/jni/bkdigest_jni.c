@@ -16,8 +16,9 @@
  *    (INTEGRATION.md §2): device count/init, per-call resume for CRC32C and CRC32, host-memory
  *    batches, and the host-resident DigestManager verify/package batches.
  *
- * Built only where a JDK is present (native/jni/Makefile; this image has none). Every C function it
- * calls is exercised through ctypes in tests/ (test_native_host.py, test_gpu_*.py).
+ * Built into a loadable library only where a JDK is present (native/jni/Makefile; this image has
+ * none). The CPU suite compiles this file with -Wall -Werror against a test-only <jni.h>
+ * (tests/jni_fake/) and calls every native through a fake JNIEnv (tests/test_jni_shim.py).
  */
 #include <jni.h>
 #include <stdint.h>
@@ -45,24 +46,32 @@ JNIEXPORT jint JNICALL Java_com_scurrilous_circe_crc_Sse42Crc32C_nativeArray(JNI
     (void)cls;
     (void)config;
     if (length <= 0) return current;
-    if ((uint64_t)length > bkd_get_cpu_route_max() && bkd_device_count() > 0) {
-        /* the GPU route (a PCIe round trip): copy the region out instead of holding the array's
-         * critical section, which stalls the JVM's collector, across it (the reference held it only
-         * for a CPU scan, crc32c_sse42_jni.cpp:29-31) */
+    const int long_route = (uint64_t)length > bkd_get_cpu_route_max();
+    if (long_route) {
+        /* past the per-call CPU bound (the GPU route, a PCIe round trip, or a multi-MiB scan over
+         * the host pool): copy the region out instead of holding the array's critical section, which
+         * stalls the JVM's collector, across it (the reference held it only for a short CPU scan,
+         * crc32c_sse42_jni.cpp:29-31). An index/length outside the array leaves the JVM's
+         * ArrayIndexOutOfBoundsException pending and returns 0. */
         jbyte* copy = (jbyte*)malloc((size_t)length);
-        if (!copy) return 0;
-        (*env)->GetByteArrayRegion(env, input, index, length, copy);
-        jint crc = 0;
-        if (!(*env)->ExceptionCheck(env)) crc = resume_host_or_zero(current, copy, length);
-        free(copy);
-        return crc;
+        if (copy) {
+            (*env)->GetByteArrayRegion(env, input, index, length, copy);
+            jint crc = 0;
+            if (!(*env)->ExceptionCheck(env)) crc = resume_host_or_zero(current, copy, length);
+            free(copy);
+            return crc;
+        }
+        /* no memory for the copy: the CPU route inside the critical section instead (never a bare 0
+         * that a caller could take for a checksum) */
     }
     /* the CPU route: pinned for the duration of the scan only, as crc32c_sse42_jni.cpp:29-31 */
     jbyte* buf = (jbyte*)(*env)->GetPrimitiveArrayCritical(env, input, 0);
-    if (!buf) return 0;
-    const jint crc = resume_host_or_zero(current, buf + index, length);
+    if (!buf) return 0; /* the JVM's OutOfMemoryError is pending */
+    uint32_t out = 0;
+    const int rc = long_route ? bkd_cpu_resume(BKD_CRC32C, (uint32_t)current, buf + index, (uint64_t)length, &out)
+                              : bkd_resume_host(BKD_CRC32C, (uint32_t)current, buf + index, (uint64_t)length, &out);
     (*env)->ReleasePrimitiveArrayCritical(env, input, buf, JNI_ABORT);
-    return crc;
+    return rc == BKD_OK ? (jint)out : 0;
 }
 
 JNIEXPORT jint JNICALL Java_com_scurrilous_circe_crc_Sse42Crc32C_nativeDirectBuffer(JNIEnv* env, jclass cls,
