@@ -40,13 +40,11 @@ static jint resume_host_or_zero(jint current, const void* p, jlong length) {
     return bkd_resume_host(BKD_CRC32C, (uint32_t)current, p, (uint64_t)length, &out) == BKD_OK ? (jint)out : 0;
 }
 
-JNIEXPORT jint JNICALL Java_com_scurrilous_circe_crc_Sse42Crc32C_nativeArray(JNIEnv* env, jclass cls, jint current,
-                                                                             jbyteArray input, jint index,
-                                                                             jint length, jlong config) {
-    (void)cls;
-    (void)config;
+/* A heap array's region [index, index + length) (nativeArray and GpuDigest.resumeArray). */
+static jint array_resume(JNIEnv* env, int algo, jint current, jbyteArray input, jint index, jint length) {
     if (length <= 0) return current;
     const int long_route = (uint64_t)length > bkd_get_cpu_route_max();
+    uint32_t out = 0;
     if (long_route) {
         /* past the per-call CPU bound (the GPU route, a PCIe round trip, or a multi-MiB scan over
          * the host pool): copy the region out instead of holding the array's critical section, which
@@ -56,10 +54,10 @@ JNIEXPORT jint JNICALL Java_com_scurrilous_circe_crc_Sse42Crc32C_nativeArray(JNI
         jbyte* copy = (jbyte*)malloc((size_t)length);
         if (copy) {
             (*env)->GetByteArrayRegion(env, input, index, length, copy);
-            jint crc = 0;
-            if (!(*env)->ExceptionCheck(env)) crc = resume_host_or_zero(current, copy, length);
+            int rc = BKD_ERR_BOUNDS;
+            if (!(*env)->ExceptionCheck(env)) rc = bkd_resume_host(algo, (uint32_t)current, copy, (uint64_t)length, &out);
             free(copy);
-            return crc;
+            return rc == BKD_OK ? (jint)out : 0;
         }
         /* no memory for the copy: the CPU route inside the critical section instead (never a bare 0
          * that a caller could take for a checksum) */
@@ -67,11 +65,18 @@ JNIEXPORT jint JNICALL Java_com_scurrilous_circe_crc_Sse42Crc32C_nativeArray(JNI
     /* the CPU route: pinned for the duration of the scan only, as crc32c_sse42_jni.cpp:29-31 */
     jbyte* buf = (jbyte*)(*env)->GetPrimitiveArrayCritical(env, input, 0);
     if (!buf) return 0; /* the JVM's OutOfMemoryError is pending */
-    uint32_t out = 0;
-    const int rc = long_route ? bkd_cpu_resume(BKD_CRC32C, (uint32_t)current, buf + index, (uint64_t)length, &out)
-                              : bkd_resume_host(BKD_CRC32C, (uint32_t)current, buf + index, (uint64_t)length, &out);
+    const int rc = long_route ? bkd_cpu_resume(algo, (uint32_t)current, buf + index, (uint64_t)length, &out)
+                              : bkd_resume_host(algo, (uint32_t)current, buf + index, (uint64_t)length, &out);
     (*env)->ReleasePrimitiveArrayCritical(env, input, buf, JNI_ABORT);
     return rc == BKD_OK ? (jint)out : 0;
+}
+
+JNIEXPORT jint JNICALL Java_com_scurrilous_circe_crc_Sse42Crc32C_nativeArray(JNIEnv* env, jclass cls, jint current,
+                                                                             jbyteArray input, jint index,
+                                                                             jint length, jlong config) {
+    (void)cls;
+    (void)config;
+    return array_resume(env, BKD_CRC32C, current, input, index, length);
 }
 
 JNIEXPORT jint JNICALL Java_com_scurrilous_circe_crc_Sse42Crc32C_nativeDirectBuffer(JNIEnv* env, jclass cls,
@@ -138,6 +143,16 @@ JNIEXPORT jint JNICALL Java_org_apache_bookkeeper_proto_checksum_GpuDigest_resum
     return bkd_resume_host(algo, (uint32_t)current, (const void*)(intptr_t)address, (uint64_t)len, &out) == BKD_OK
                ? (jint)out
                : 0;
+}
+
+/* resumeArray(algo, current, byte[], offset, len): a heap buffer (ByteBuf.array()); the Java side has
+ * checked the bounds (AbstractIncrementalIntHash.java:62-69) */
+JNIEXPORT jint JNICALL Java_org_apache_bookkeeper_proto_checksum_GpuDigest_resumeArray(JNIEnv* env, jclass cls,
+                                                                                     jint algo, jint current,
+                                                                                     jbyteArray input, jint offset,
+                                                                                     jint len) {
+    (void)cls;
+    return array_resume(env, algo, current, input, offset, len);
 }
 
 /* batch over one host region: offsets/lengths/seeds/out are addresses of direct buffers */

@@ -74,6 +74,7 @@ def shim(tmp_path_factory):
         GPU + "deviceCount": (i32, [vp, vp]),
         GPU + "init": (i32, [vp, vp, i32]),
         GPU + "resumeAddress": (i32, [vp, vp, i32, i32, i64, i64]),
+        GPU + "resumeArray": (i32, [vp, vp, i32, i32, vp, i32, i32]),
         GPU + "resumeBatch": (i32, [vp, vp, i32, i64, i64, i64, i64, i64, i64, i32, i64]),
         GPU + "verifyBatch": (i64, [vp, vp, i32, i64, i64, ctypes.c_uint8, i64, i64, i64, i64]),
         GPU + "packageBatch": (i32, [vp, vp, i32, i64, i64, i64, i64, i64, i64, i64, i64, i64, i64]),
@@ -149,6 +150,24 @@ def test_native_array_copy_out_route(shim, env):
     assert f(env, None, 0, arr, 0, 16, 0) == 0
     assert shim.fake_pending().startswith(b"java/lang/OutOfMemoryError")
     shim.fake_clear()
+    shim.fake_free(arr)
+
+
+def test_gpu_digest_resume_array(shim, env):
+    """GpuDigest.resumeArray (GpuIntHash's heap-buffer path) for both polynomials, on both branches."""
+    L = _native.lib()
+    data = np.random.default_rng(18).bytes(30000)
+    arr = _barray(shim, data)
+    f = getattr(shim, GPU + "resumeArray")
+    for algo in (CRC32C, CRC32):
+        assert f(env, None, algo, 0, arr, 0, 9) == _jint(oracle.calculate(algo, data[:9]))
+        assert f(env, None, algo, 0x99, arr, 17, 29000) == _jint(oracle.resume(algo, 0x99, data[17:29017]))
+        assert f(env, None, algo, 0x99, arr, 17, 0) == 0x99
+        L.bkd_set_cpu_route_max(ctypes.c_uint64(1024))
+        try:
+            assert f(env, None, algo, 0x99, arr, 17, 29000) == _jint(oracle.resume(algo, 0x99, data[17:29017]))
+        finally:
+            L.bkd_set_cpu_route_max(ctypes.c_uint64(0xFFFFFFFFFFFFFFFF))
     shim.fake_free(arr)
 
 

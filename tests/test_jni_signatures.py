@@ -32,6 +32,7 @@ GPU_DIGEST = [
     ("int", "deviceCount", []),
     ("int", "init", ["int"]),
     ("int", "resumeAddress", ["int", "int", "long", "long"]),
+    ("int", "resumeArray", ["int", "int", "byte[]", "int", "int"]),
     ("int", "resumeBatch", ["int", "long", "long", "long", "long", "long", "long", "int", "long"]),
     ("long", "verifyBatch", ["int", "long", "long", "boolean", "long", "long", "long", "long"]),
     ("int", "packageBatch", ["int", "long", "long", "long", "long", "long", "long", "long", "long", "long", "long"]),
@@ -79,3 +80,15 @@ def test_sse42_natives_match_reference_declarations(name):
     assert m.group(1) == ret
     got = [p.strip().rsplit(" ", 1)[0] for p in m.group(2).split(",") if p.strip()]
     assert got == params
+
+
+def test_gpu_digest_java_declarations_match_table():
+    """native/java/.../GpuDigest.java (the committed Java side of the batch class) declares exactly the
+    natives of the table, with the same types, so the shim, the table and the Java source agree."""
+    src = os.path.join(ROOT, "native", "java", "org", "apache", "bookkeeper", "proto", "checksum", "GpuDigest.java")
+    text = re.sub(r"/\*.*?\*/", "", open(src).read(), flags=re.S)
+    found = {}
+    for m in re.finditer(r"public static native (\S+) (\w+)\(([^)]*)\);", text, flags=re.S):
+        params = [p.strip().rsplit(" ", 1)[0] for p in m.group(3).split(",") if p.strip()]
+        found[m.group(2)] = (m.group(1), params)
+    assert found == {name: (ret, params) for ret, name, params in GPU_DIGEST}
