@@ -655,7 +655,9 @@ struct StagePool {
     std::vector<std::unique_ptr<HostStage>> all;
     std::vector<HostStage*> idle;
 };
-StagePool g_stages[kMaxDevices];
+// Deliberately never destroyed: static destructors run after HIP's own teardown, where
+// hipHostFree / hipStreamDestroy can crash or hang at exit; bkd_host_release frees idle sets instead.
+StagePool* const g_stages = new StagePool[kMaxDevices];
 
 size_t max_stages() {
     static const size_t m = [] {
@@ -1403,6 +1405,13 @@ int bkd_crc_batch_host(int algo, const void* h_base, uint64_t base_size, const u
             ++j;
         } while (left);
     }
+    // the pipeline walks offsets in order: an entry that starts inside a long entry's later pieces
+    // (overlapping entries are legal, only bounds are checked) breaks that order, so such a
+    // batch takes the one-copy route instead
+    for (uint64_t j = 1; j < m; ++j)
+        if (off2[j] < off2[j - 1])
+            return host_batch_oneshot(*ds, hs, algo, (const uint8_t*)h_base, base_size, h_offsets, h_lengths, n,
+                                      h_seeds, seed_all, h_out);
     rc = host_batch_pipelined(*ds, hs, algo, (const uint8_t*)h_base, off2.data(), len2.data(), m, seed2.data(), 0,
                               out2.data());
     if (rc) return rc;

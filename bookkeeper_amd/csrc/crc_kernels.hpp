@@ -115,6 +115,13 @@ constexpr uint64_t kLowClockMHz = BKD_LOW_CLOCK_MHZ;
 // the kernel's LDS image (its only __shared__ array, at LDS address 0: the byte addresses v_perm
 // builds are absolute), followed by one s_waitcnt that takes every result as an operand, so no use
 // can be scheduled before it.
+// fold4_main is valid only while the table image really sits at LDS address 0 (another
+// __shared__ variable in a kernel that uses it could move the image): the kernels take it only when
+// this holds, otherwise they keep the compiler's schedule (same digests, mul_main_add).
+__device__ __forceinline__ bool lds_image_at_zero(const uint32_t* lds) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t*)lds == 0u;
+}
+
 __device__ __forceinline__ void fold4_main(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t lanereg,
                                            uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3) {
     uint32_t t[16];
@@ -875,8 +882,9 @@ __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __res
     const uint64_t clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
     stage_tables<G>(lds, tables);
     const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
-    const bool low_clock = sched == 2 || (sched == 0 && BKD_CLOCK_ADAPT &&
-                                          (clk1 - clk0) * 100u < (rt1 - rt0) * (uint64_t)kLowClockMHz);
+    const bool low_clock = lds_image_at_zero(lds) &&
+                           (sched == 2 || (sched == 0 && BKD_CLOCK_ADAPT &&
+                                           (clk1 - clk0) * 100u < (rt1 - rt0) * (uint64_t)kLowClockMHz));
 
     const int lane = threadIdx.x & 63;
     const int g = lane & (G - 1);
@@ -1071,18 +1079,11 @@ __device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lan
     uint32_t fx = 0u;
     if (d0 > Gm::kStep - 4) fx = place_seed(r0, d0 - Gm::kStep);
     uint32_t c0 = w.x, c1 = w.y, c2 = w.z, c3 = w.w;
-    // long chunk with a pad in this lane's last block: that block again, requested now (its line is
-    // in cache by the time it is used), instead of selecting it among the A/B sets afterwards
-    // (Zipf -0.5 % in both A/B orders)
-    u32x4 relast = u32x4{0u, 0u, 0u, 0u};
-#if BKD_TAIL_UNCOND
-    // requested by every long chunk (the lane's last block, always inside the window), so that the
-    // number of loads in flight does not depend on the pad and the waits stay exact
-    if (rem > (uint32_t)PF) relast = ld16<false>(base + a + (int64_t)rem * Gm::kStep);
-#else
-    if (rem > (uint32_t)PF && c.pad && c.keep < 16) relast = ld16<false>(base + a + (int64_t)rem * Gm::kStep);
-#endif
-#define BKD_FOLD0(d)                                     \
+    // the lane's last block as it was folded: a pad is XORed out of the very register that folded
+    // it, so the bytes past the entry (another entry's, or past the caller's buffer) cancel whatever
+    // they hold, even if something rewrites them while the chunk runs (no second load of that block)
+    u32x4 last = W0;
+#define BKD_FOLD0(d)                                    \
     do {                                                 \
         c0 = mul_main_add(lds, c0, lanereg, (d).x ^ fx);    \
         fx = 0u;                                         \
@@ -1105,6 +1106,9 @@ __device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lan
 #pragma unroll
         for (int k = 1; k < PF; ++k)
             if ((uint32_t)k < rem) BKD_FOLD(A[k]);
+#pragma unroll
+        for (int k = 0; k < PF; ++k)
+            if ((uint32_t)k + 1u == rem) last = A[k];
     } else {
         const uint8_t* p = base + a + (int64_t)(PF + 1) * Gm::kStep;  // first step not yet loaded
         uint32_t left = rem - (uint32_t)PF;
@@ -1124,29 +1128,19 @@ __device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lan
             p += (int64_t)(2 * PF) * Gm::kStep;
             left -= 2u * PF;
         }
-#if BKD_TAIL_UNCOND
-#pragma unroll
-        for (int k = 0; k < PF; ++k) B[k] = ld16<NT>(p + (int64_t)std::min<int32_t>(k, (int32_t)left - 1) * Gm::kStep);
-        asm volatile("" ::: "memory");  // keeps the loads here: not sunk into the conditional folds
-#else
+        // (the A/B tail loads stay conditional here: with clamped unconditional loads the last block
+        // would be requested twice, and the pad must come out of the register that folded it)
 #pragma unroll
         for (int k = 0; k < PF; ++k)
             if ((uint32_t)k < left) B[k] = ld16<NT>(p + (int64_t)k * Gm::kStep);
-#endif
         if (first) BKD_FOLD0(A[0]);
         else BKD_FOLD(A[0]);
 #pragma unroll
         for (int k = 1; k < PF; ++k) BKD_FOLD(A[k]);
-#if BKD_TAIL_UNCOND
-#pragma unroll
-        for (int k = 0; k < PF; ++k)
-            A[k] = ld16<NT>(p + (int64_t)std::min<int32_t>(PF + k, (int32_t)left - 1) * Gm::kStep);
-        asm volatile("" ::: "memory");
-#else
+        last = A[PF - 1];  // the last block when left == 0 (A is reloaded below only for steps < left)
 #pragma unroll
         for (int k = 0; k < PF; ++k)
             if ((uint32_t)(PF + k) < left) A[k] = ld16<NT>(p + (int64_t)(PF + k) * Gm::kStep);
-#endif
 #if !BKD_EARLY_PREFETCH
         chunk_prefetch<G, PF, NT>(base, nx, NW0, NA);  // issued after every load of this chunk
 #endif
@@ -1156,31 +1150,23 @@ __device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lan
 #pragma unroll
         for (int k = 0; k < PF; ++k)
             if ((uint32_t)(PF + k) < left) BKD_FOLD(A[k]);
+#pragma unroll
+        for (int k = 0; k < PF; ++k) {
+            if ((uint32_t)k + 1u == left) last = B[k];
+            if ((uint32_t)(PF + k) + 1u == left) last = A[k];
+        }
     }
 #undef BKD_FOLD
 #undef BKD_FOLD0
-    if (c.pad) {
-        // the last step's block of this lane ends past the entry: its bytes >= the entry's end
-        // were folded last (XORed in after the final multiply), so XOR them out again
-        if (c.keep < 16) {
-            u32x4 last;
-            if (rem == 0u) {
-                last = W0;
-            } else if (rem <= (uint32_t)PF) {
-                last = A[0];
-#pragma unroll
-                for (int k = 1; k < PF; ++k)
-                    if ((uint32_t)k == rem - 1u) last = A[k];
-            } else {
-                last = relast;
-            }
-            const int32_t keep = c.keep;
-            const u32x4 junk = keep <= 0 ? last : mask_low_bytes(last, (uint32_t)keep);
-            c0 ^= junk.x;
-            c1 ^= junk.y;
-            c2 ^= junk.z;
-            c3 ^= junk.w;
-        }
+    if (c.pad && c.keep < 16) {
+        // the last step's block of this lane ends past the entry: its bytes >= the entry's end were
+        // folded last (XORed in after the final multiply), so XOR them out again
+        const int32_t keep = c.keep;
+        const u32x4 junk = keep <= 0 ? last : mask_low_bytes(last, (uint32_t)keep);
+        c0 ^= junk.x;
+        c1 ^= junk.y;
+        c2 ^= junk.z;
+        c3 ^= junk.w;
     }
     return finish_lanes<G>(lds, c0, c1, c2, c3);
 }
@@ -1580,8 +1566,9 @@ __global__ void __launch_bounds__(kBlock) crc_verify_fused_kernel(
     const uint64_t clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
     stage_tables<G>(lds, tables);
     const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
-    const bool low_clock = sched == 2 || (sched == 0 && BKD_CLOCK_ADAPT &&
-                                          (clk1 - clk0) * 100u < (rt1 - rt0) * (uint64_t)kLowClockMHz);
+    const bool low_clock = lds_image_at_zero(lds) &&
+                           (sched == 2 || (sched == 0 && BKD_CLOCK_ADAPT &&
+                                           (clk1 - clk0) * 100u < (rt1 - rt0) * (uint64_t)kLowClockMHz));
     const int lane = threadIdx.x & 63;
     const int g = lane & (G - 1);
     const uint32_t lanereg = ((uint32_t)(lane & 31) << 2) | (1u << 16);
