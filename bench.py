@@ -98,6 +98,23 @@ def gather_over_ranks(values: list[float], device=None) -> list[list[float]]:
     return [o.cpu().tolist() for o in out]
 
 
+def gather_identity(dev, world: int) -> list[dict]:
+    """Each rank's device identity (name, PCI address, UUID) and the world size it saw after
+    init_process_group, gathered to every rank: a multi-GPU line names the GPUs it ran on."""
+    import torch
+    import torch.distributed as dist
+    p = torch.cuda.get_device_properties(dev)
+    mine = {"device": p.name, "gcn_arch": getattr(p, "gcnArchName", ""),
+            "pci": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}",
+            "uuid": str(getattr(p, "uuid", "")),
+            "world_size_seen": dist.get_world_size() if (dist.is_available() and dist.is_initialized()) else 1}
+    if world == 1 or not (dist.is_available() and dist.is_initialized()):
+        return [mine]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, mine)
+    return out
+
+
 def max_over_ranks(value: float, device=None) -> float:
     """Whole-job time = the slowest rank's (all_reduce MAX; the only cross-rank traffic)."""
     import torch
@@ -649,6 +666,12 @@ def run_rank(args, ck, torch, dist, world: int, rank: int, dev) -> None:
     coll_dev = dev if args.dist_backend == "nccl" else None
     elapsed_max = max_over_ranks(elapsed, coll_dev)
     per_rank = gather_over_ranks([elapsed, avg_kernel_s, solo_kernel_s or avg_kernel_s], coll_dev)
+    idents = gather_identity(dev, world)
+    if world > 1 and args.dist_backend == "nccl" and rank == 0:
+        # a SCALE line must come from N distinct GPUs: one PCI address per rank under RCCL
+        pcis = [d["pci"] for d in idents]
+        if len(set(pcis)) != len(pcis):
+            raise SystemExit(f"ranks share a GPU under nccl: {pcis}")
 
     total_payload = payload_bytes * world * args.steps  # every rank processes its batch once per step
     value = total_payload / elapsed_max / GIB
@@ -677,7 +700,7 @@ def run_rank(args, ck, torch, dist, world: int, rank: int, dev) -> None:
         # per GPU: its own wall rate over the timed region, its kernel time, and (N > 1) its rate when
         # it ran alone on the node in this same run; efficiency = (aggregate / N) / mean solo rate
         "per_gpu": [{"rank": r, "GiB_s": round(payload_bytes * args.steps / e / GIB, 2),
-                     "kernel_ms": round(k * 1e3, 4), "solo_GiB_s": round(payload_bytes / so / GIB, 2)}
+                     "kernel_ms": round(k * 1e3, 4), "solo_GiB_s": round(payload_bytes / so / GIB, 2), **idents[r]}
                     for r, (e, k, so) in enumerate(per_rank)],
         "per_gpu_GiB_s": round(value / world, 2),
     }

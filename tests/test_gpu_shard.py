@@ -153,6 +153,11 @@ def test_bench_two_ranks_default_is_config4_shard(gpu):
     assert len(res["per_gpu"]) == 2
     for p in res["per_gpu"]:
         assert p["GiB_s"] > 0 and p["solo_GiB_s"] > 0 and p["kernel_ms"] > 0
+        # each rank names its GPU and the world it joined (equal PCI addresses are
+        # expected here: gloo on one card; under nccl rank 0 refuses equal ones)
+        assert p["world_size_seen"] == 2 and p["device"] and p["uuid"] is not None
+        assert len(p["pci"].split(":")) == 3
+    assert [p["rank"] for p in res["per_gpu"]] == [0, 1]
     # whole-job value = both ranks' payload over the slowest rank's time
     total = 2 * 8388608 * 4096 * res["steps"] / (1 << 30)
     assert abs(res["value"] - total / (res["ms_per_step"] * res["steps"] / 1e3)) / res["value"] < 0.01
