@@ -384,7 +384,7 @@ def set_fold_schedule(schedule: int) -> None:
 
 
 def set_plan_mode(mode: int) -> None:
-    """0 = auto, 1 = one entry per lane group, 2 = chunked plan (indexed batches)."""
+    """0 = auto, 1 = one entry per lane group, 2 = chunked plan, 3 = stream route (indexed batches)."""
     check(lib().bkd_set_plan_mode(mode))
 
 

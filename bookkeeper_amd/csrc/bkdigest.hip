@@ -73,6 +73,7 @@ struct StreamScratch {
     // PlanRun word of the plans enqueued on this stream and the epoch of the latest one
     uint32_t* run = nullptr;
     uint32_t* uni = nullptr;  // PlanRun uniform-lengths word (the epoch of the call it holds for)
+    uint32_t* sword = nullptr;  // stream-route word (StreamArgs::word: the epoch of the call that takes it)
     uint32_t epoch = 0;
     // verify gate word (verify_gate_kernel) and the epoch of the latest verify on this stream
     uint32_t* vflag = nullptr;
@@ -111,6 +112,18 @@ struct StreamScratch {
             }
         }
         *out = uni;
+        return hipSuccess;
+    }
+    hipError_t stream_word(hipStream_t st, uint32_t** out) {
+        if (!sword) {
+            hipError_t e = hipMalloc((void**)&sword, sizeof(uint32_t));
+            if (e == hipSuccess) e = hipMemsetAsync(sword, 0, sizeof(uint32_t), st);
+            if (e != hipSuccess) {
+                sword = nullptr;
+                return e;
+            }
+        }
+        *out = sword;
         return hipSuccess;
     }
     hipError_t flag(hipStream_t st, uint32_t** out) {
@@ -169,6 +182,7 @@ struct DeviceState {
     int cus = 0;
     uint32_t* tables[2][kNumLaneChoices] = {};  // [algo][lane choice] compact operator images
     uint32_t* xinv[2] = {};       // [algo] x^(-8k), k = 0..127: removes the plan's zero padding
+    uint32_t* xline[2] = {};      // [algo] x^(1024 L), L = 0..32: the stream route's last piece of L lines
     std::shared_mutex maps_mu;    // guards xtab and scratch
     std::map<uint64_t, uint32_t*> xtab;  // (algo, CH) -> x^(8*CH) operator for the plan's combine
     std::map<hipStream_t, std::unique_ptr<StreamScratch>> scratch;
@@ -177,7 +191,7 @@ struct DeviceState {
 std::mutex g_mu;  // device initialisation only
 DeviceState g_dev[kMaxDevices];
 std::atomic<int> g_forced_lanes{0};
-std::atomic<int> g_plan_mode{0};  // 0 auto, 1 direct (one entry per group), 2 chunked plan
+std::atomic<int> g_plan_mode{0};  // 0 auto, 1 direct (one entry per group), 2 chunked plan, 3 stream route
 
 // Chunked plan geometry (bkd_set_plan_geometry): lanes per group, steps per full chunk
 // (CH = 16 * lanes * jc bytes) and the head-merge threshold in bytes.
@@ -268,6 +282,10 @@ int init_device_locked(int dev) {
         for (uint32_t k = 0; k < 128; ++k) inv[k] = bkd::gf2::xpow_neg8(algo, k);
         BKD_HIP(hipMalloc(&ds.xinv[algo], sizeof(inv)));
         BKD_HIP(hipMemcpy(ds.xinv[algo], inv, sizeof(inv), hipMemcpyHostToDevice));
+        uint32_t xl[bkd::kTileLines + 1];
+        for (uint32_t k = 0; k <= bkd::kTileLines; ++k) xl[k] = bkd::gf2::xpow(algo, 1024ull * k);
+        BKD_HIP(hipMalloc(&ds.xline[algo], sizeof(xl)));
+        BKD_HIP(hipMemcpy(ds.xline[algo], xl, sizeof(xl), hipMemcpyHostToDevice));
     }
     BKD_HIP(hipSetDevice(prev));
     ds.ready.store(true, std::memory_order_release);
@@ -393,17 +411,17 @@ template <int G>
 void launch_plan_chunks(const bkd::PlanRun& run, const uint8_t* base, const bkd::PlanDesc* descs,
                         const uint32_t* count, const uint32_t* tab,
                         uint32_t* out, uint32_t* partials, const bkd::PlanDirectSrc& ov, int blocks, hipStream_t st,
-                        uint32_t* err, int pf) {
+                        uint32_t* err, int pf, const bkd::StreamArgs& sa, const uint32_t* xinv, uint32_t poly) {
     // pf: read once by launch_plan (one value per call)
     if (pf == 8)
         hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 8, kNT, bkd::PlanDirectSrc>), dim3((unsigned)blocks),
-                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err);
+                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err, sa, xinv, poly);
     else if (pf == 4)
         hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 4, kNT, bkd::PlanDirectSrc>), dim3((unsigned)blocks),
-                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err);
+                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err, sa, xinv, poly);
     else
         hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 2, kNT, bkd::PlanDirectSrc>), dim3((unsigned)blocks),
-                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err);
+                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err, sa, xinv, poly);
 }
 
 // Indexed batch through the chunked plan (plan_kernels.hpp): five stream-ordered kernels, no
@@ -417,6 +435,8 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     if (n == 0) return BKD_OK;
     if (ext_flag) short_class = direct_gate = false;
     if (n >= 0xFFFFFFF0ull) return fail(BKD_ERR_INVALID_ARG, "indexed batches hold fewer than 2^32 - 16 entries");
+    const int mode = g_plan_mode.load();
+    if (mode == 3) short_class = false;  // the stream route forced: every entry is the stream's
     const int G = g_plan_lanes.load();
     bkd::PlanGeo pg;
     pg.step = 16u * (uint32_t)G;
@@ -447,12 +467,22 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     const uint64_t capacity = std::min<uint64_t>(n + (size + 128u * n) / pg.ch + 16, 0xFFFFFFF0ull);
     const uint32_t nb = (uint32_t)((n + bkd::kPlanBlock - 1) / bkd::kPlanBlock);
     const uint32_t ncols = bkd::plan_ncols(pg);
+    // The stream route: tiles of 32 lines of 8-lane steps, joined with x^(8 * 4096) —
+    // the plan's own operator at its default geometry. Decided on the device by plan_scan (at most
+    // jumps_max entries that do not continue their predecessor's lines; forced: any number).
+    const bool stream = BKD_STREAM && (mode == 0 || mode == 3) && G == 8 && pg.ch == 4096u && pg.small == 0u;
+    // tiles: non-overlapping entries span at most size / 128 + 2 n lines, each jump wastes < 1 tile
+    const uint64_t tcap = stream ? (size / 128u + 2u * n) / bkd::kTileLines + n + 16u : 0u;
     Carver cv;
     const size_t o_blk = cv.take((size_t)nb * ncols * 4), o_live = cv.take((size_t)nb * 4),
                  o_bok = cv.take((size_t)nb * 4),
                  o_blkoff = cv.take((size_t)nb * ncols * 4), o_hdr = cv.take(bkd::kHdrWords * 4),
                  o_ps = cv.take((size_t)n * 4), o_hs = cv.take((size_t)n * 4), o_part = cv.take((size_t)capacity * 4),
                  o_desc = cv.take((size_t)capacity * sizeof(bkd::PlanDesc));
+    const size_t o_sblk = cv.take(stream ? (size_t)nb * 24 : 0), o_sbase = cv.take(stream ? (size_t)nb * 8 : 0),
+                 o_shdr = cv.take(stream ? 32 : 0), o_spos = cv.take(stream ? (size_t)n * 8 : 0),
+                 o_srec = cv.take(stream ? (size_t)n * 16 : 0), o_tf = cv.take((size_t)tcap * 4),
+                 o_tk = cv.take((size_t)tcap * 4), o_pf = cv.take((size_t)tcap * 4), o_pl = cv.take((size_t)tcap * 4);
     StreamScratch& sc = scratch_for(ds, st);
     std::lock_guard<std::recursive_mutex> lk(sc.mu);
     uint8_t* sb = nullptr;
@@ -471,9 +501,28 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     if (e == hipSuccess) e = sc.flag(st, &err);
     if (e == hipSuccess && pg.small) e = sc.run_word(st, &run_word);
     if (e == hipSuccess && gate) e = sc.uni_word(st, &uni);
+    uint32_t* sword = nullptr;
+    if (e == hipSuccess && stream) e = sc.stream_word(st, &sword);
     if (e != hipSuccess) return fail(BKD_ERR_NOMEM, std::string("plan scratch: ") + hipGetErrorString(e));
     if (++sc.epoch == 0u) ++sc.epoch;  // 0 is the words' initial value
     const bkd::PlanRun run = ext_flag ? bkd::PlanRun{ext_flag, nullptr, ext_epoch} : bkd::PlanRun{run_word, uni, sc.epoch};
+    bkd::StreamArgs sa{};
+    if (stream) {
+        sa.sblk = Carver::at<uint64_t>(sb, o_sblk);
+        sa.sbase = Carver::at<uint64_t>(sb, o_sbase);
+        sa.shdr = Carver::at<uint64_t>(sb, o_shdr);
+        sa.spos = Carver::at<uint64_t>(sb, o_spos);
+        sa.srec = Carver::at<bkd::u32x4>(sb, o_srec);
+        sa.tfirst = Carver::at<uint32_t>(sb, o_tf);
+        sa.tk0 = Carver::at<uint32_t>(sb, o_tk);
+        sa.pfirst = Carver::at<uint32_t>(sb, o_pf);
+        sa.plast = Carver::at<uint32_t>(sb, o_pl);
+        sa.cap = tcap;
+        sa.jumps_max = mode == 3 ? UINT64_MAX : n / 64u + 1u;
+        sa.mis = pg.mis;
+        sa.word = sword;
+        sa.epoch = sc.epoch;
+    }
     uint32_t *blk = Carver::at<uint32_t>(sb, o_blk), *blive = Carver::at<uint32_t>(sb, o_live),
              *bok = gate ? Carver::at<uint32_t>(sb, o_bok) : nullptr,
              *blkoff = Carver::at<uint32_t>(sb, o_blkoff), *hdr = Carver::at<uint32_t>(sb, o_hdr),
@@ -494,26 +543,30 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
 #endif
     const uint32_t pgrid = BKD_PLAN_GRID ? (uint32_t)BKD_PLAN_GRID * (uint32_t)ds.cus : 0xFFFFFFFFu;
     hipLaunchKernelGGL(bkd::plan_count_kernel, dim3(std::min(nb, pgrid)), dim3(bkd::kPlanBlock), 0, st, offsets,
-                       lengths, size, n, pg, blk, blive, nb, run, bok);
-    hipLaunchKernelGGL(bkd::plan_scan_kernel, dim3(ncols + (gate ? 1u : 0u)), dim3(bkd::kPlanBlock), 0, st, blk, nb,
-                       blkoff, hdr, run, ncols, bok);
+                       lengths, size, n, pg, blk, blive, nb, run, bok, sa);
+    hipLaunchKernelGGL(bkd::plan_scan_kernel, dim3(ncols + (gate ? 1u : 0u) + (stream ? 1u : 0u)),
+                       dim3(bkd::kPlanBlock), 0, st, blk, nb, blkoff, hdr, run, ncols, bok, sa);
     // few entry blocks (large entries): replicate emit and combine blocks so ~2 blocks per CU work
     const uint32_t reps = nb >= 2u * (uint32_t)ds.cus ? 1u : std::min<uint32_t>(64u, (2u * (uint32_t)ds.cus + nb - 1u) / nb);
     hipLaunchKernelGGL(bkd::plan_emit_kernel, dim3(std::min(nb * reps, pgrid)), dim3(bkd::kPlanBlock), 0, st, offsets,
-                       lengths, seeds, seed_all, size, n, pg, capacity, blkoff, pslot, hslot, hdr, descs, reps, blive, nb, run);
+                       lengths, seeds, seed_all, size, n, pg, capacity, blkoff, pslot, hslot, hdr, descs, reps, blive, nb, run,
+                       sa);
     const uint32_t* tab = ds.tables[algo][lane_index(G)];
     const bkd::PlanDirectSrc ov{n, offsets, lengths, seeds, seed_all, size, out, pslot, hdr, capacity, false};
     switch (G) {
-        case 4: launch_plan_chunks<4>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
-        case 8: launch_plan_chunks<8>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
-        case 16: launch_plan_chunks<16>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
-        case 32: launch_plan_chunks<32>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
-        default: launch_plan_chunks<64>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
+        case 4: launch_plan_chunks<4>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf, sa, ds.xinv[algo], bkd::gf2::poly(algo)); break;
+        case 8: launch_plan_chunks<8>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf, sa, ds.xinv[algo], bkd::gf2::poly(algo)); break;
+        case 16: launch_plan_chunks<16>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf, sa, ds.xinv[algo], bkd::gf2::poly(algo)); break;
+        case 32: launch_plan_chunks<32>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf, sa, ds.xinv[algo], bkd::gf2::poly(algo)); break;
+        default: launch_plan_chunks<64>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf, sa, ds.xinv[algo], bkd::gf2::poly(algo)); break;
     }
+    if (stream)
+        hipLaunchKernelGGL((bkd::crc_stream_tiles_kernel<kNT>), dim3(ds.cus), dim3(bkd::kBlock), 0, st, base, size, n,
+                           tab, out, run, sa, ds.xinv[algo], bkd::gf2::poly(algo));
     const uint32_t* btab = tab + bkd::gf2::byte_table_offset(G);
     hipLaunchKernelGGL(bkd::plan_combine_kernel, dim3(std::min(nb * reps, pgrid)), dim3(1024), 0, st, base, offsets, lengths, seeds,
                        seed_all, size, n, pg, xtab, bkd::gf2::xpow(algo, 8ull * pg.ch), btab, ds.xinv[algo],
-                       bkd::gf2::poly(algo), pslot, hslot, partials, out, err, reps, blive, nb, run);
+                       bkd::gf2::poly(algo), pslot, hslot, partials, out, err, reps, blive, nb, run, sa, ds.xline[algo]);
     e = hipGetLastError();
     if (e != hipSuccess) return fail(BKD_ERR_HIP, std::string("plan kernels: ") + hipGetErrorString(e));
     return BKD_OK;
@@ -523,7 +576,7 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
 bool indexed_direct(uint64_t size) {
     const int mode = g_plan_mode.load();
     // plan descriptors hold a biased 41-bit window start (PlanDesc): buffers >= 1 TiB take the direct kernel
-    return mode == 1 || (mode == 0 && size <= kDirectMaxBytes) || size >= bkd::kPlanMaxSize;
+    return mode == 1 || (mode == 0 && size <= kDirectMaxBytes) || size >= bkd::kPlanMaxSize;  // (3: stream)
 }
 
 // route: -1 decided here from the plan mode and the buffer size, else the caller's decision
@@ -1207,7 +1260,8 @@ int bkd_set_group_lanes(int lanes) {
 }
 
 int bkd_set_plan_mode(int mode) {
-    if (mode < 0 || mode > 2) return fail(BKD_ERR_INVALID_ARG, "plan mode must be 0 (auto), 1 (direct) or 2 (plan)");
+    if (mode < 0 || mode > 3)
+        return fail(BKD_ERR_INVALID_ARG, "plan mode must be 0 (auto), 1 (direct), 2 (plan) or 3 (stream)");
     g_plan_mode.store(mode);
     return BKD_OK;
 }
@@ -1345,7 +1399,7 @@ int bkd_stream_release(void* stream) {
         BKD_HIP(hipStreamSynchronize(st));  // the stream's own work is done with them
         for (int k = 0; k < 3; ++k)
             if (sc->buf[k]) BKD_HIP(hipFree(sc->buf[k]));
-        for (uint32_t* w : {sc->err, sc->run, sc->uni, sc->vflag})
+        for (uint32_t* w : {sc->err, sc->run, sc->uni, sc->vflag, sc->sword})
             if (w) BKD_HIP(hipFree(w));
         if (sc->h_err) BKD_HIP(hipHostFree(sc->h_err));
     }

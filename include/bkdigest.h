@@ -274,8 +274,10 @@ BKD_API uint32_t bkd_host_xpow8n(int algo, uint64_t nbytes);
 
 /* Tuning: lanes per entry group (0 = automatic, else 1/4/8/16/32/64); prefetch is fixed at build. */
 BKD_API int bkd_set_group_lanes(int lanes);
-/* Indexed-batch strategy: 0 = automatic (chunked plan unless the base buffer is <= 256 KiB),
- * 1 = one entry per lane group, 2 = always the chunked plan. */
+/* Indexed-batch strategy: 0 = automatic (unless the base buffer is <= 256 KiB: the stream route when
+ * the device finds the entries laid out in order (at most n/64 + 1 of them not continuing their
+ * predecessor's lines), else the chunked plan), 1 = one entry per lane group, 2 = always the chunked
+ * plan, 3 = always the stream route. */
 BKD_API int bkd_set_plan_mode(int mode);
 /* Chunked-plan geometry: lanes per group (4, 8, 16, 32 or 64), steps per full chunk (chunk = 16 * lanes *
  * steps bytes, <= 32 KiB) and the head-merge threshold in bytes (a head chunk shorter than this

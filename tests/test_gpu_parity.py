@@ -100,7 +100,7 @@ def test_golden_vectors(gpu):
         assert (got == want).all(), lanes
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
 def test_golden_batch_4096(gpu, mode):
     """SURVEY.md §8c's 4096-entry reference-generated set (lengths 0..70000, unaligned offsets into
     a 32 MiB stream, seeded) through the automatic route, the direct kernel and the chunk plan."""
@@ -247,10 +247,11 @@ def test_uniform_tiny_entries_auto_one_lane(gpu):
 
 
 @pytest.mark.parametrize("algo", [ck.CRC32C, ck.CRC32])
-@pytest.mark.parametrize("lanes,mode", [(l, 1) for l in LANES] + [(0, 2), (0, 0)])
+@pytest.mark.parametrize("lanes,mode", [(l, 1) for l in LANES] + [(0, 2), (0, 0), (0, 3)])
 def test_indexed_ragged_unaligned(gpu, algo, lanes, mode):
     """Random lengths 0..70000, random (unaligned, overlapping) offsets, random per-entry seeds;
-    mode 1 = one entry per lane group, mode 2 = chunked plan, mode 0 = automatic."""
+    mode 1 = one entry per lane group, mode 2 = chunked plan, mode 0 = automatic, 3 = stream route
+    (every entry a jump here: one tile run each)."""
     import torch
     ck.set_group_lanes(lanes)
     ck.set_plan_mode(mode)
@@ -747,7 +748,7 @@ def test_zipf_full_size_every_entry_vs_reference(gpu):
     try:
         for algo in (ck.CRC32C, ck.CRC32):
             want, _ = _threaded_reference(algo, host, offs, lens)
-            for mode in (0, 2, 1):  # auto (the bench's route), chunked plan, direct
+            for mode in (0, 2, 1, 3):  # auto (the bench's route: stream), chunked plan, direct, stream
                 ck.set_plan_mode(mode)
                 got = ck.crc_batch(algo, base, d_off, d_len, sync_check=True).cpu().numpy().view(np.uint32)
                 bad = np.nonzero(got != want)[0]
