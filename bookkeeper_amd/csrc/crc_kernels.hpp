@@ -1403,12 +1403,10 @@ __device__ __forceinline__ void stream_link(const SEnt& p, const SEnt& e, bool& 
 
 // Keeps bytes [a, b) of a 16-byte block (block coordinates, any range), zeroes the rest.
 __device__ __forceinline__ u32x4 keep_range(u32x4 w, int32_t a, int32_t b) {
-    auto m = [](uint32_t x, int32_t lo, int32_t hi) -> uint32_t {
-        lo = lo < 0 ? 0 : lo;
-        hi = hi > 4 ? 4 : hi;
-        if (hi <= lo) return 0u;
-        const uint32_t mh = hi >= 4 ? 0xFFFFFFFFu : ((1u << (8 * hi)) - 1u);
-        return x & mh & (0xFFFFFFFFu << (8 * lo));
+    auto m = [](uint32_t x, int32_t lo, int32_t hi) -> uint32_t {  // (selects, no branches)
+        const int32_t a = lo < 0 ? 0 : lo, b = hi > 4 ? 4 : hi, wd = b - a;
+        const uint32_t msk = (0xFFFFFFFFu >> ((uint32_t)(32 - 8 * wd) & 31u)) << ((uint32_t)(8 * a) & 31u);
+        return wd > 0 ? x & msk : 0u;
     };
     w.x = m(w.x, a, b);
     w.y = m(w.y, a - 4, b - 4);
@@ -1445,9 +1443,12 @@ __device__ __forceinline__ SRel srel(const u32x4& r, uint64_t L0, uint64_t size,
 
 // The tiles of the stream in grid stride, one per 8-lane group per round of kTileLines steps; four
 // register sets hold the next four lines (the last steps of a round load the next tile's first
-// lines). A tile's index words are read two rounds ahead and its first two entry records one round
-// ahead, all at fixed points of the round, so every load is unconditional except an entry record at
-// an entry change.
+// lines). Every load is unconditional, at a fixed point of the round, so that the compiler's memory
+// waits stay counted (no drain of the lines in flight): a tile's index words two rounds ahead, the
+// records of its first two entries one round ahead, and after every step the record of the entry
+// after the current one (an entry change in the next step takes it from there; a second change
+// within one line, entries of under a line side by side, loads its record on the spot). Rounds are
+// unrolled by two with the record registers' roles swapped, so nothing loaded is copied.
 template <bool NT>
 __device__ __forceinline__ void stream_tiles_loop(const uint32_t* lds, uint32_t lanereg, int g,
                                                   const uint8_t* __restrict__ base, uint64_t size,
@@ -1470,117 +1471,142 @@ __device__ __forceinline__ void stream_tiles_loop(const uint32_t* lds, uint32_t 
         return t < ntiles ? (uint32_t)(end - t * TL < TL ? end - t * TL : TL) : 1u;
     };
 
+    // tile state: this round's (t, tf, k0) and the next round's (t1, tf1, k01); records of the first
+    // two entries of a tile in (RA, RB) / (RA1, RB1), the roles swapping between the two unrolled rounds
     uint64_t t = gid;
-    uint32_t tf = sa.tfirst[clampt(t)];
-    uint32_t k0 = sa.tk0[clampt(t)];
-    u32x4 r = ld_rec(tf), rn = ld_rec(tf + 1u);  // the tile's first entry and the one after it
+    uint32_t tf = sa.tfirst[clampt(t)], k0 = sa.tk0[clampt(t)];
+    u32x4 PA = ld_rec(tf), PB = ld_rec(tf + 1u);
     uint64_t t1 = t + ngroups;
     uint32_t tf1 = sa.tfirst[clampt(t1)], k01 = sa.tk0[clampt(t1)];
-    u32x4 ra1 = ld_rec(tf1), rb1 = ld_rec(tf1 + 1u);
-    uint64_t L0 = first_line(r, k0);
+    u32x4 QA = ld_rec(tf1), QB = ld_rec(tf1 + 1u);
+    uint64_t L0 = first_line(PA, k0);
     uint32_t nl = lines_of(t);
     u32x4 X0 = ld_line(L0), X1 = ld_line(L0 + (1u < nl ? 1u : nl - 1u)), X2 = ld_line(L0 + (2u < nl ? 2u : nl - 1u)),
           X3 = ld_line(L0 + (3u < nl ? 3u : nl - 1u));
-    while (__any(t < ntiles)) {  // wave-uniform: a group past the last tile runs empty rounds
-        const bool act = t < ntiles;
-        uint32_t i = tf;
-        SRel e = srel(r, L0, size, mis);
-        uint32_t r0 = ~r.w;
-        bool from_start = k0 == 0u, fresh = true, live = act;
-        uint32_t c0 = 0u, c1 = 0u, c2 = 0u, c3 = 0u;
-        const uint32_t nla = act ? nl : 0u;  // lines this group folds in this round
-        const uint64_t t2 = t1 + ngroups;
-        const uint32_t tf2 = sa.tfirst[clampt(t2)], k02 = sa.tk0[clampt(t2)];
-        uint64_t L1 = 0u;
-        uint32_t nl1 = 1u;
-        // device line of step s of this round (s >= TL: the next tile's); past the tile's end the
-        // last line again (an L2 hit), never a line outside the buffer
-        auto line_of = [&](uint32_t s) -> uint64_t {
-            return s < TL ? L0 + (s < nl ? s : nl - 1u) : L1 + (s - TL < nl1 ? s - TL : nl1 - 1u);
-        };
-#define BKD_STREAM_STEP(XS, S)                                                                        \
-        {                                                                                             \
-            const uint32_t s_ = (S);                                                                  \
-            const u32x4 w = XS;                                                                       \
-            XS = ld_line(line_of(s_ + 4u));                                                           \
-            bool more = live && s_ < nla;                                                             \
-            while (__any(more)) {                                                                     \
-                if (more) {                                                                           \
-                    const int32_t sv = (int32_t)s_;                                                   \
-                    const int32_t lbase = 128 * sv + 16 * g;                                          \
-                    u32x4 wm = w;                                                                     \
-                    if (sv == e.sF || sv == e.sL) wm = keep_range(w, e.a - lbase, e.e - lbase);       \
-                    if (sv == e.sF) {                                                                 \
-                        const int64_t dd = (int64_t)e.d - 16 * g;                                     \
-                        wm.x ^= place_seed(r0, dd);                                                   \
-                        wm.y ^= place_seed(r0, dd - 4);                                               \
-                        wm.z ^= place_seed(r0, dd - 8);                                               \
-                        wm.w ^= place_seed(r0, dd - 12);                                              \
+    u32x4 R0, R1;  // the record of the entry after the current one, loaded after each step (even / odd)
+
+#define BKD_STREAM_STEP(XS, S, RUSE, RLOAD)                                                           \
+    {                                                                                                 \
+        const uint32_t s_ = (S);                                                                      \
+        const u32x4 w = XS;                                                                           \
+        bool more = live && s_ < nla;                                                                 \
+        bool first_change = true;                                                                     \
+        while (__any(more)) {                                                                         \
+            if (more) {                                                                               \
+                const int32_t sv = (int32_t)s_;                                                       \
+                const int32_t lbase = 128 * sv + 16 * g;                                              \
+                u32x4 wm = w;                                                                         \
+                if (sv == e.sF || sv == e.sL) wm = keep_range(w, e.a - lbase, e.e - lbase);           \
+                if (sv == e.sF) {                                                                     \
+                    const int64_t dd = (int64_t)e.d - 16 * g;                                         \
+                    wm.x ^= place_seed(r0, dd);                                                       \
+                    wm.y ^= place_seed(r0, dd - 4);                                                   \
+                    wm.z ^= place_seed(r0, dd - 8);                                                   \
+                    wm.w ^= place_seed(r0, dd - 12);                                                  \
+                }                                                                                     \
+                if (sv == e.sF + 1 && e.d > 124u && g == 0) wm.x ^= place_seed(r0, (int64_t)e.d - 128); \
+                const uint32_t m0 = mul_main_add(lds, c0, lanereg, wm.x);                             \
+                const uint32_t m1 = mul_main_add(lds, c1, lanereg, wm.y);                             \
+                const uint32_t m2 = mul_main_add(lds, c2, lanereg, wm.z);                             \
+                const uint32_t m3 = mul_main_add(lds, c3, lanereg, wm.w);                             \
+                c0 = fresh ? wm.x : m0;                                                               \
+                c1 = fresh ? wm.y : m1;                                                               \
+                c2 = fresh ? wm.z : m2;                                                               \
+                c3 = fresh ? wm.w : m3;                                                               \
+                fresh = false;                                                                        \
+                more = false;                                                                         \
+                if (sv == e.sL) { /* the entry ends in this line */                                  \
+                    const uint32_t reg = finish_lanes<8>(lds, c0, c1, c2, c3);                        \
+                    if (g == 0) {                                                                     \
+                        if (from_start) out[i] = ~(e.pad ? gf_mul_bits(xinv[e.pad], reg, poly) : reg); \
+                        else sa.pfirst[t] = reg;                                                      \
                     }                                                                                 \
-                    if (sv == e.sF + 1 && e.d > 124u && g == 0) wm.x ^= place_seed(r0, (int64_t)e.d - 128); \
-                    const uint32_t m0 = mul_main_add(lds, c0, lanereg, wm.x);                         \
-                    const uint32_t m1 = mul_main_add(lds, c1, lanereg, wm.y);                         \
-                    const uint32_t m2 = mul_main_add(lds, c2, lanereg, wm.z);                         \
-                    const uint32_t m3 = mul_main_add(lds, c3, lanereg, wm.w);                         \
-                    c0 = fresh ? wm.x : m0;                                                           \
-                    c1 = fresh ? wm.y : m1;                                                           \
-                    c2 = fresh ? wm.z : m2;                                                           \
-                    c3 = fresh ? wm.w : m3;                                                           \
-                    fresh = false;                                                                    \
-                    more = false;                                                                     \
-                    if (sv == e.sL) { /* the entry ends in this line */                              \
-                        const uint32_t reg = finish_lanes<8>(lds, c0, c1, c2, c3);                    \
-                        if (g == 0) {                                                                 \
-                            if (from_start) out[i] = ~(e.pad ? gf_mul_bits(xinv[e.pad], reg, poly) : reg); \
-                            else sa.pfirst[t] = reg;                                                  \
-                        }                                                                             \
-                        fresh = true;                                                                 \
-                        from_start = true;                                                            \
-                        const bool pin = e.in;                                                        \
-                        const int32_t psL = e.sL;                                                     \
-                        ++i;                                                                          \
-                        e = srel(rn, L0, size, mis);                                                  \
-                        r0 = ~rn.w;                                                                   \
-                        rn = ld_rec(i + 1u);                                                          \
-                        const bool sh = pin && e.sF == psL, cont = pin && (sh || e.sF == psL + 1);    \
-                        if (i >= n || !e.in || !cont) live = false; /* a jump: a new tile */          \
-                        else more = sh; /* it starts in this same line */                            \
+                    fresh = true;                                                                     \
+                    from_start = true;                                                                \
+                    const bool pin = e.in;                                                            \
+                    const int32_t psL = e.sL;                                                         \
+                    ++i;                                                                              \
+                    /* the next entry's record: loaded after the previous step, or (a second */      \
+                    /* change in this line) now */                                                    \
+                    u32x4 rq = RUSE;                                                                  \
+                    if (!first_change) { /* rare: waits for its own load, so the common path's */    \
+                        rq = ld_rec(i);  /* counted waits are not disturbed */                        \
+                        asm volatile("s_waitcnt vmcnt(0)" : "+v"(rq.x), "+v"(rq.y), "+v"(rq.z), "+v"(rq.w)); \
                     }                                                                                 \
+                    first_change = false;                                                             \
+                    e = srel(rq, L0, size, mis);                                                      \
+                    r0 = ~rq.w;                                                                       \
+                    const bool sh = pin && e.sF == psL, cont = pin && (sh || e.sF == psL + 1);        \
+                    if (i >= n || !e.in || !cont) live = false; /* a jump: a new tile */              \
+                    else more = sh; /* it starts in this same line */                                \
                 }                                                                                     \
             }                                                                                         \
-            if (live && !fresh && s_ + 1u == nla) { /* the tile ends inside entry i */               \
-                const uint32_t reg = finish_lanes<8>(lds, c0, c1, c2, c3);                            \
-                if (g == 0) {                                                                         \
-                    if (from_start) sa.plast[t] = reg;                                                \
-                    else sa.pfirst[t] = reg;                                                          \
-                }                                                                                     \
+        }                                                                                             \
+        if (live && !fresh && s_ + 1u == nla) { /* the tile ends inside entry i */                   \
+            const uint32_t reg = finish_lanes<8>(lds, c0, c1, c2, c3);                                \
+            if (g == 0) {                                                                             \
+                if (from_start) sa.plast[t] = reg;                                                    \
+                else sa.pfirst[t] = reg;                                                              \
             }                                                                                         \
-        }
-        for (uint32_t s0 = 0; s0 < TL; s0 += 4u) {
-            if (s0 + 4u == TL) {  // the next tile's first lines are loaded from here on
-                L1 = first_line(ra1, k01);
-                nl1 = lines_of(t1);
-            }
-            BKD_STREAM_STEP(X0, s0)
-            BKD_STREAM_STEP(X1, s0 + 1u)
-            BKD_STREAM_STEP(X2, s0 + 2u)
-            BKD_STREAM_STEP(X3, s0 + 3u)
-        }
-#undef BKD_STREAM_STEP
-        // the next tile
-        t = t1;
-        tf = tf1;
-        k0 = k01;
-        r = ra1;
-        rn = rb1;
-        L0 = L1;
-        nl = nl1;
-        t1 = t2;
-        tf1 = tf2;
-        k01 = k02;
-        ra1 = ld_rec(tf1);
-        rb1 = ld_rec(tf1 + 1u);
+        }                                                                                             \
+        /* the record first, then the line: a change in the next step then waits for the record */ \
+        /* and the older lines only, never for the line just requested; the line set is refilled */  \
+        /* once its line is folded (the same registers: no copy at the loop's back edge) */          \
+        RLOAD = ld_rec(i + 1u);                                                                       \
+        XS = ld_line(line_of(s_ + 4u));                                                               \
     }
+
+    // One round: the tile (t, tf, k0) with records (RA, RB); the next tile's records are in (NA, NB)
+    // already, and the round ends by loading the records of the tile after it into (RA, RB).
+#define BKD_STREAM_ROUND(RA, RB, NA, NB)                                                              \
+    {                                                                                                 \
+        const bool act = t < ntiles;                                                                  \
+        uint32_t i = tf;                                                                              \
+        SRel e = srel(RA, L0, size, mis);                                                             \
+        uint32_t r0 = ~RA.w;                                                                          \
+        bool from_start = k0 == 0u, fresh = true, live = act;                                         \
+        uint32_t c0 = 0u, c1 = 0u, c2 = 0u, c3 = 0u;                                                  \
+        const uint32_t nla = act ? nl : 0u;                                                           \
+        const uint64_t t2 = t1 + ngroups;                                                             \
+        const uint32_t tf2 = sa.tfirst[clampt(t2)], k02 = sa.tk0[clampt(t2)];                         \
+        uint64_t L1 = 0u;                                                                             \
+        uint32_t nl1 = 1u;                                                                            \
+        auto line_of = [&](uint32_t s) -> uint64_t {                                                  \
+            return s < TL ? L0 + (s < nl ? s : nl - 1u) : L1 + (s - TL < nl1 ? s - TL : nl1 - 1u);    \
+        };                                                                                            \
+        BKD_STREAM_STEP(X0, 0u, RB, R0)                                                               \
+        BKD_STREAM_STEP(X1, 1u, R0, R1)                                                               \
+        BKD_STREAM_STEP(X2, 2u, R1, R0)                                                               \
+        BKD_STREAM_STEP(X3, 3u, R0, R1)                                                               \
+        for (uint32_t s0 = 4u; s0 < TL; s0 += 4u) {                                                   \
+            if (s0 + 4u == TL) { /* the next tile's first lines are loaded from here on */           \
+                L1 = first_line(NA, k01);                                                             \
+                nl1 = lines_of(t1);                                                                   \
+            }                                                                                         \
+            BKD_STREAM_STEP(X0, s0, R1, R0)                                                           \
+            BKD_STREAM_STEP(X1, s0 + 1u, R0, R1)                                                      \
+            BKD_STREAM_STEP(X2, s0 + 2u, R1, R0)                                                      \
+            BKD_STREAM_STEP(X3, s0 + 3u, R0, R1)                                                      \
+        }                                                                                             \
+        t = t1;                                                                                       \
+        tf = tf1;                                                                                     \
+        k0 = k01;                                                                                     \
+        L0 = L1;                                                                                      \
+        nl = nl1;                                                                                     \
+        t1 = t2;                                                                                      \
+        tf1 = tf2;                                                                                    \
+        k01 = k02;                                                                                    \
+        RA = ld_rec(tf1);                                                                             \
+        RB = ld_rec(tf1 + 1u);                                                                        \
+    }
+    for (;;) {  // wave-uniform: a group past the last tile runs empty rounds until its wave is done
+        BKD_STREAM_ROUND(PA, PB, QA, QB)
+        if (!__any(t < ntiles)) break;
+        BKD_STREAM_ROUND(QA, QB, PA, PB)
+        if (!__any(t < ntiles)) break;
+    }
+#undef BKD_STREAM_ROUND
+#undef BKD_STREAM_STEP
 }
 
 // Chunk kernel of the ragged-batch plan: one chunk per group, grid stride over the descriptor
