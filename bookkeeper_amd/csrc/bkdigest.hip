@@ -470,7 +470,9 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     // The stream route: tiles of 32 lines of 8-lane steps, joined with x^(8 * 4096) —
     // the plan's own operator at its default geometry. Decided on the device by plan_scan (at most
     // jumps_max entries that do not continue their predecessor's lines; forced: any number).
-    const bool stream = BKD_STREAM && (mode == 0 || mode == 3) && G == 8 && pg.ch == 4096u && pg.small == 0u;
+    // (the tile kernel numbers lines, tiles and entries in 32 bits)
+    const bool stream = BKD_STREAM && (mode == 0 || mode == 3) && G == 8 && pg.ch == 4096u && pg.small == 0u &&
+                        size < (1ull << 38) && n < (1ull << 30);
     // tiles: non-overlapping entries span at most size / 128 + 2 n lines, each jump wastes < 1 tile
     const uint64_t tcap = stream ? (size / 128u + 2u * n) / bkd::kTileLines + n + 16u : 0u;
     Carver cv;

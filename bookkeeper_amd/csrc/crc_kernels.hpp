@@ -1106,9 +1106,11 @@ __device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lan
 #pragma unroll
         for (int k = 1; k < PF; ++k)
             if ((uint32_t)k < rem) BKD_FOLD(A[k]);
+        if (c.pad && c.keep < 16) {  // (selected only where a pad is removed: no cost per full chunk)
 #pragma unroll
-        for (int k = 0; k < PF; ++k)
-            if ((uint32_t)k + 1u == rem) last = A[k];
+            for (int k = 0; k < PF; ++k)
+                if ((uint32_t)k + 1u == rem) last = A[k];
+        }
     } else {
         const uint8_t* p = base + a + (int64_t)(PF + 1) * Gm::kStep;  // first step not yet loaded
         uint32_t left = rem - (uint32_t)PF;
@@ -1150,10 +1152,12 @@ __device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lan
 #pragma unroll
         for (int k = 0; k < PF; ++k)
             if ((uint32_t)(PF + k) < left) BKD_FOLD(A[k]);
+        if (c.pad && c.keep < 16) {
 #pragma unroll
-        for (int k = 0; k < PF; ++k) {
-            if ((uint32_t)k + 1u == left) last = B[k];
-            if ((uint32_t)(PF + k) + 1u == left) last = A[k];
+            for (int k = 0; k < PF; ++k) {
+                if ((uint32_t)k + 1u == left) last = B[k];
+                if ((uint32_t)(PF + k) + 1u == left) last = A[k];
+            }
         }
     }
 #undef BKD_FOLD
@@ -1444,53 +1448,58 @@ __device__ __forceinline__ SRel srel(const u32x4& r, uint64_t L0, uint64_t size,
 // The tiles of the stream in grid stride, one per 8-lane group per round of kTileLines steps; four
 // register sets hold the next four lines (the last steps of a round load the next tile's first
 // lines). Every load is unconditional, at a fixed point of the round, so that the compiler's memory
-// waits stay counted (no drain of the lines in flight): a tile's index words two rounds ahead, the
-// records of its first two entries one round ahead, and after every step the record of the entry
-// after the current one (an entry change in the next step takes it from there; a second change
-// within one line, entries of under a line side by side, loads its record on the spot). Rounds are
-// unrolled by two with the record registers' roles swapped, so nothing loaded is copied.
+// waits stay counted (no drain of the lines in flight): the next tile's index words and first
+// record one round ahead, and beside every line a window of the eight records after the current
+// entry, one per lane (`W`, base index `B`), used four steps later like the line itself: an entry
+// change takes its record from the window with a group shuffle. Only when more than eight entries
+// began within five lines (entries of under half a line) is a record loaded on the spot, on a path
+// that waits for itself. A record loaded one step ahead instead made every entry change wait for
+// it and for the three lines before it: mixed 1 KiB entries 2x slower, Zipf 2.4x (profiles/r04c_*).
+// The loop body is the four steps of one line set, so the hot loop stays small in the instruction
+// cache. An entry's digest leaves here raw; plan_combine applies x^(-8 pad) and the inversion.
 template <bool NT>
 __device__ __forceinline__ void stream_tiles_loop(const uint32_t* lds, uint32_t lanereg, int g,
                                                   const uint8_t* __restrict__ base, uint64_t size,
                                                   const StreamArgs& sa, uint64_t n, uint64_t gid, uint64_t ngroups,
-                                                  uint32_t* __restrict__ out, const uint32_t* __restrict__ xinv,
-                                                  uint32_t poly) {
+                                                  uint32_t* __restrict__ out) {
     constexpr uint32_t TL = kTileLines;
-    const uint64_t end = sa.shdr[0], ntiles = sa.shdr[1];
+    // line and tile numbers fit 32 bits (launch_plan takes the stream route below 2^38 bytes)
+    const uint32_t end = (uint32_t)sa.shdr[0], ntiles = (uint32_t)sa.shdr[1];
     if (ntiles == 0u || size == 0u) return;  // (kernel-uniform)
     const uint8_t* lb = base - sa.mis;  // device line 0 (the line holding base)
-    const uint64_t lmax = ((uint64_t)sa.mis + size - 1u) >> 7;
+    const uint32_t lmax = (uint32_t)(((uint64_t)sa.mis + size - 1u) >> 7);
     const uint32_t mis = sa.mis;
-    auto ld_line = [&](uint64_t L) { return ld16<NT>(lb + ((L < lmax ? L : lmax) << 7) + 16 * g); };
+    auto ld_line = [&](uint32_t L) { return ld16<NT>(lb + ((uint64_t)(L < lmax ? L : lmax) << 7) + 16 * g); };
     auto ld_rec = [&](uint64_t i) { return sa.srec[i < n ? i : n - 1u]; };
-    auto first_line = [&](const u32x4& r, uint32_t k) {
-        return (((uint64_t)mis + ((uint64_t)r.x | ((uint64_t)r.y << 32))) >> 7) + k;
+    auto first_line = [&](const u32x4& r, uint32_t k) -> uint32_t {
+        return (uint32_t)(((uint64_t)mis + ((uint64_t)r.x | ((uint64_t)r.y << 32))) >> 7) + k;
     };
-    auto clampt = [&](uint64_t t) { return t < ntiles ? t : ntiles - 1u; };
-    auto lines_of = [&](uint64_t t) -> uint32_t {
-        return t < ntiles ? (uint32_t)(end - t * TL < TL ? end - t * TL : TL) : 1u;
-    };
+    auto clampt = [&](uint32_t t) { return t < ntiles ? t : ntiles - 1u; };
+    auto lines_of = [&](uint32_t t) -> uint32_t { return t < ntiles ? (end - t * TL < TL ? end - t * TL : TL) : 1u; };
+    const uint32_t ng = (uint32_t)ngroups;
 
-    // tile state: this round's (t, tf, k0) and the next round's (t1, tf1, k01); records of the first
-    // two entries of a tile in (RA, RB) / (RA1, RB1), the roles swapping between the two unrolled rounds
-    uint64_t t = gid;
+    // this round's tile (t, tf, k0) and the next round's (t1, tf1, k01); RA: the first record of
+    // this tile at a round's start, of the next tile from then on
+    uint32_t t = (uint32_t)gid;
     uint32_t tf = sa.tfirst[clampt(t)], k0 = sa.tk0[clampt(t)];
-    u32x4 PA = ld_rec(tf), PB = ld_rec(tf + 1u);
-    uint64_t t1 = t + ngroups;
+    u32x4 RA = ld_rec(tf);
+    // record windows: lane g of the group holds record B + g
+    uint32_t B0 = tf + 1u, B1 = B0, B2 = B0, B3 = B0;
+    const int lane8 = (int)(threadIdx.x & 56u);  // the group's first lane in its wave
+    u32x4 W0 = ld_rec((uint64_t)B0 + g), W1 = ld_rec((uint64_t)B0 + g), W2 = ld_rec((uint64_t)B0 + g),
+          W3 = ld_rec((uint64_t)B0 + g);
+    uint32_t t1 = t + ng;
     uint32_t tf1 = sa.tfirst[clampt(t1)], k01 = sa.tk0[clampt(t1)];
-    u32x4 QA = ld_rec(tf1), QB = ld_rec(tf1 + 1u);
-    uint64_t L0 = first_line(PA, k0);
+    uint32_t L0 = first_line(RA, k0);
     uint32_t nl = lines_of(t);
     u32x4 X0 = ld_line(L0), X1 = ld_line(L0 + (1u < nl ? 1u : nl - 1u)), X2 = ld_line(L0 + (2u < nl ? 2u : nl - 1u)),
           X3 = ld_line(L0 + (3u < nl ? 3u : nl - 1u));
-    u32x4 R0, R1;  // the record of the entry after the current one, loaded after each step (even / odd)
 
-#define BKD_STREAM_STEP(XS, S, RUSE, RLOAD)                                                           \
+#define BKD_STREAM_STEP(XS, WS, BS, S)                                                                \
     {                                                                                                 \
         const uint32_t s_ = (S);                                                                      \
         const u32x4 w = XS;                                                                           \
         bool more = live && s_ < nla;                                                                 \
-        bool first_change = true;                                                                     \
         while (__any(more)) {                                                                         \
             if (more) {                                                                               \
                 const int32_t sv = (int32_t)s_;                                                       \
@@ -1515,10 +1524,10 @@ __device__ __forceinline__ void stream_tiles_loop(const uint32_t* lds, uint32_t 
                 c3 = fresh ? wm.w : m3;                                                               \
                 fresh = false;                                                                        \
                 more = false;                                                                         \
-                if (sv == e.sL) { /* the entry ends in this line */                                  \
+                if (sv == e.sL) { /* the entry ends in this line: its raw register */                \
                     const uint32_t reg = finish_lanes<8>(lds, c0, c1, c2, c3);                        \
                     if (g == 0) {                                                                     \
-                        if (from_start) out[i] = ~(e.pad ? gf_mul_bits(xinv[e.pad], reg, poly) : reg); \
+                        if (from_start) out[i] = reg;                                                 \
                         else sa.pfirst[t] = reg;                                                      \
                     }                                                                                 \
                     fresh = true;                                                                     \
@@ -1526,86 +1535,79 @@ __device__ __forceinline__ void stream_tiles_loop(const uint32_t* lds, uint32_t 
                     const bool pin = e.in;                                                            \
                     const int32_t psL = e.sL;                                                         \
                     ++i;                                                                              \
-                    /* the next entry's record: loaded after the previous step, or (a second */      \
-                    /* change in this line) now */                                                    \
-                    u32x4 rq = RUSE;                                                                  \
-                    if (!first_change) { /* rare: waits for its own load, so the common path's */    \
-                        rq = ld_rec(i);  /* counted waits are not disturbed */                        \
+                    /* the next entry's record: from the window loaded four steps ago, or (more */   \
+                    /* than eight entries since) loaded now on a path that waits for itself */        \
+                    const uint32_t k = i - BS;                                                        \
+                    u32x4 rq;                                                                         \
+                    if (k < 8u) {                                                                     \
+                        const int src = lane8 + (int)k;                                                 \
+                        rq.x = (uint32_t)__shfl((int)WS.x, src);                                      \
+                        rq.y = (uint32_t)__shfl((int)WS.y, src);                                      \
+                        rq.z = (uint32_t)__shfl((int)WS.z, src);                                      \
+                        rq.w = (uint32_t)__shfl((int)WS.w, src);                                      \
+                    } else {                                                                          \
+                        rq = ld_rec(i);                                                               \
                         asm volatile("s_waitcnt vmcnt(0)" : "+v"(rq.x), "+v"(rq.y), "+v"(rq.z), "+v"(rq.w)); \
                     }                                                                                 \
-                    first_change = false;                                                             \
                     e = srel(rq, L0, size, mis);                                                      \
                     r0 = ~rq.w;                                                                       \
                     const bool sh = pin && e.sF == psL, cont = pin && (sh || e.sF == psL + 1);        \
                     if (i >= n || !e.in || !cont) live = false; /* a jump: a new tile */              \
-                    else more = sh; /* it starts in this same line */                                \
+                    else more = sh; /* it starts in this same line */                                 \
                 }                                                                                     \
             }                                                                                         \
         }                                                                                             \
-        if (live && !fresh && s_ + 1u == nla) { /* the tile ends inside entry i */                   \
-            const uint32_t reg = finish_lanes<8>(lds, c0, c1, c2, c3);                                \
-            if (g == 0) {                                                                             \
-                if (from_start) sa.plast[t] = reg;                                                    \
-                else sa.pfirst[t] = reg;                                                              \
-            }                                                                                         \
-        }                                                                                             \
-        /* the record first, then the line: a change in the next step then waits for the record */ \
-        /* and the older lines only, never for the line just requested; the line set is refilled */  \
-        /* once its line is folded (the same registers: no copy at the loop's back edge) */          \
-        RLOAD = ld_rec(i + 1u);                                                                       \
+        /* the window first, then the line (a change four steps on waits for neither the line */    \
+        /* just requested nor the ones after it); both refill the registers just used (no copy */    \
+        /* at the loop's back edge). The round's last four steps load the next tile's window. */    \
+        BS = s_ + 4u >= TL ? tf1 + 1u : i + 1u;                                                       \
+        WS = ld_rec((uint64_t)BS + g);                                                                \
         XS = ld_line(line_of(s_ + 4u));                                                               \
     }
 
-    // One round: the tile (t, tf, k0) with records (RA, RB); the next tile's records are in (NA, NB)
-    // already, and the round ends by loading the records of the tile after it into (RA, RB).
-#define BKD_STREAM_ROUND(RA, RB, NA, NB)                                                              \
-    {                                                                                                 \
-        const bool act = t < ntiles;                                                                  \
-        uint32_t i = tf;                                                                              \
-        SRel e = srel(RA, L0, size, mis);                                                             \
-        uint32_t r0 = ~RA.w;                                                                          \
-        bool from_start = k0 == 0u, fresh = true, live = act;                                         \
-        uint32_t c0 = 0u, c1 = 0u, c2 = 0u, c3 = 0u;                                                  \
-        const uint32_t nla = act ? nl : 0u;                                                           \
-        const uint64_t t2 = t1 + ngroups;                                                             \
-        const uint32_t tf2 = sa.tfirst[clampt(t2)], k02 = sa.tk0[clampt(t2)];                         \
-        uint64_t L1 = 0u;                                                                             \
-        uint32_t nl1 = 1u;                                                                            \
-        auto line_of = [&](uint32_t s) -> uint64_t {                                                  \
-            return s < TL ? L0 + (s < nl ? s : nl - 1u) : L1 + (s - TL < nl1 ? s - TL : nl1 - 1u);    \
-        };                                                                                            \
-        BKD_STREAM_STEP(X0, 0u, RB, R0)                                                               \
-        BKD_STREAM_STEP(X1, 1u, R0, R1)                                                               \
-        BKD_STREAM_STEP(X2, 2u, R1, R0)                                                               \
-        BKD_STREAM_STEP(X3, 3u, R0, R1)                                                               \
-        for (uint32_t s0 = 4u; s0 < TL; s0 += 4u) {                                                   \
-            if (s0 + 4u == TL) { /* the next tile's first lines are loaded from here on */           \
-                L1 = first_line(NA, k01);                                                             \
-                nl1 = lines_of(t1);                                                                   \
-            }                                                                                         \
-            BKD_STREAM_STEP(X0, s0, R1, R0)                                                           \
-            BKD_STREAM_STEP(X1, s0 + 1u, R0, R1)                                                      \
-            BKD_STREAM_STEP(X2, s0 + 2u, R1, R0)                                                      \
-            BKD_STREAM_STEP(X3, s0 + 3u, R0, R1)                                                      \
-        }                                                                                             \
-        t = t1;                                                                                       \
-        tf = tf1;                                                                                     \
-        k0 = k01;                                                                                     \
-        L0 = L1;                                                                                      \
-        nl = nl1;                                                                                     \
-        t1 = t2;                                                                                      \
-        tf1 = tf2;                                                                                    \
-        k01 = k02;                                                                                    \
-        RA = ld_rec(tf1);                                                                             \
-        RB = ld_rec(tf1 + 1u);                                                                        \
-    }
     for (;;) {  // wave-uniform: a group past the last tile runs empty rounds until its wave is done
-        BKD_STREAM_ROUND(PA, PB, QA, QB)
-        if (!__any(t < ntiles)) break;
-        BKD_STREAM_ROUND(QA, QB, PA, PB)
+        const bool act = t < ntiles;
+        uint32_t i = tf;
+        SRel e = srel(RA, L0, size, mis);
+        uint32_t r0 = ~RA.w;
+        RA = ld_rec(tf1);
+        bool from_start = k0 == 0u, fresh = true, live = act;
+        uint32_t c0 = 0u, c1 = 0u, c2 = 0u, c3 = 0u;
+        const uint32_t nla = act ? nl : 0u;
+        const uint32_t t2 = t1 + ng;
+        const uint32_t tf2 = sa.tfirst[clampt(t2)], k02 = sa.tk0[clampt(t2)];
+        uint32_t L1 = 0u;
+        uint32_t nl1 = 1u;
+        auto line_of = [&](uint32_t s) -> uint32_t {
+            return s < TL ? L0 + (s < nl ? s : nl - 1u) : L1 + (s - TL < nl1 ? s - TL : nl1 - 1u);
+        };
+        for (uint32_t s0 = 0u; s0 < TL; s0 += 4u) {
+            if (s0 + 4u == TL) {  // the next tile's first lines are loaded from here on
+                L1 = first_line(RA, k01);
+                nl1 = lines_of(t1);
+            }
+            BKD_STREAM_STEP(X0, W0, B0, s0)
+            BKD_STREAM_STEP(X1, W1, B1, s0 + 1u)
+            BKD_STREAM_STEP(X2, W2, B2, s0 + 2u)
+            BKD_STREAM_STEP(X3, W3, B3, s0 + 3u)
+        }
+        if (live && !fresh) {  // the tile ends inside entry i
+            const uint32_t reg = finish_lanes<8>(lds, c0, c1, c2, c3);
+            if (g == 0) {
+                if (from_start) sa.plast[t] = reg;
+                else sa.pfirst[t] = reg;
+            }
+        }
+        t = t1;
+        tf = tf1;
+        k0 = k01;
+        L0 = L1;
+        nl = nl1;
+        t1 = t2;
+        tf1 = tf2;
+        k01 = k02;
         if (!__any(t < ntiles)) break;
     }
-#undef BKD_STREAM_ROUND
 #undef BKD_STREAM_STEP
 }
 
@@ -1656,15 +1658,15 @@ __global__ void __launch_bounds__(kBlock) crc_stream_tiles_kernel(const uint8_t*
                                                                   const uint32_t* __restrict__ xinv, uint32_t poly) {
     using Gm = Geo<8>;
     if (!run.plan_entries() || run.uniform() || !sa.on()) return;
-    // the tables, then x^(-8 pad) for pad = 0..127 (an LDS read at an entry's end, no memory wait)
-    __shared__ __attribute__((aligned(16))) uint32_t lds[Gm::kLdsWords + 128];
-    for (int k = threadIdx.x; k < 128; k += kBlock) lds[Gm::kLdsWords + k] = xinv[k];
+    (void)xinv;
+    (void)poly;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[Gm::kLdsWords];
     stage_tables<8>(lds, tables);
     const int lane = threadIdx.x & 63;
     const uint32_t lanereg = ((uint32_t)(lane & 31) << 2) | (1u << 16);
     const uint64_t ngroups = (uint64_t)gridDim.x * (kBlock / 8);
     const uint64_t gid = (uint64_t)blockIdx.x * (kBlock / 8) + (uint64_t)(threadIdx.x / 8);
-    stream_tiles_loop<NT>(lds, lanereg, lane & 7, base, size, sa, n, gid, ngroups, out, lds + Gm::kLdsWords, poly);
+    stream_tiles_loop<NT>(lds, lanereg, lane & 7, base, size, sa, n, gid, ngroups, out);
 }
 
 // ---- synthetic input: little-endian splitmix64 stream ----

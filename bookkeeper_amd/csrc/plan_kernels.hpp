@@ -187,10 +187,18 @@ __device__ __forceinline__ SFun sf_shfl_up(const SFun& x, int d) {
     y.b = (uint64_t)__shfl_up((unsigned long long)x.b, d);
     return y;
 }
-// The element of entry i for the position scan; `sh` / `J1` its shared flag and new lines.
+// The element of entry i for the position scan; `sh` / `J1` its shared flag and new lines. (o, l):
+// entry i's offset and length, already loaded (any value when i >= n); the predecessor's come from
+// the neighbouring lane (lane 0 loads them). Called by all threads of the wave.
 __device__ __forceinline__ SFun stream_elem(const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ lengths,
-                                            uint64_t i, uint64_t n, uint64_t size, uint32_t mis, SEnt& e, bool& sh,
-                                            bool& jp, uint64_t& J1) {
+                                            uint64_t i, uint64_t n, uint64_t size, uint32_t mis, uint64_t o, uint32_t l,
+                                            SEnt& e, bool& sh, bool& jp, uint64_t& J1) {
+    uint64_t po = (uint64_t)__shfl_up((unsigned long long)o, 1);
+    uint32_t pl = (uint32_t)__shfl_up((int)l, 1);
+    if ((threadIdx.x & 63u) == 0u && i > 0u && i - 1u < n) {
+        po = offsets[i - 1u];
+        pl = lengths[i - 1u];
+    }
     sh = false;
     jp = false;
     J1 = 0u;
@@ -198,18 +206,44 @@ __device__ __forceinline__ SFun stream_elem(const uint64_t* __restrict__ offsets
         e.in = false;
         return sf_id();
     }
-    e = stream_ent(offsets[i], lengths[i], size, mis);
+    e = stream_ent(o, l, size, mis);
     if (!e.in) return sf_id();
     SEnt p;
     p.in = false;
-    if (i > 0) p = stream_ent(offsets[i - 1], lengths[i - 1], size, mis);
+    if (i > 0) p = stream_ent(po, pl, size, mis);
     stream_link(p, e, sh, jp);
     J1 = (e.Lst - e.F + 1u) - (sh ? 1u : 0u);
     return SFun{jp ? 1u : 0u, 0u, J1};
 }
 // In-order block scan (1024 threads): this thread's inclusive composition; `total` the block's.
+// A block without a jump (every f = 0, the common case of a packed batch) composes by addition.
 __device__ __forceinline__ SFun block_scan_sf(SFun x, SFun* wt, SFun& total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (!__syncthreads_or((int)x.f)) {
+        uint64_t v = x.b;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t y = (uint64_t)__shfl_up((unsigned long long)v, d);
+            if (lane >= d) v += y;
+        }
+        if (lane == 63) wt[wave].b = v;
+        __syncthreads();
+        if (threadIdx.x < 64) {  // wave 0 scans the wave totals
+            uint64_t w = lane < kPlanBlock / 64 ? wt[lane].b : 0u, c = w;
+#pragma unroll
+            for (int d = 1; d < kPlanBlock / 64; d <<= 1) {
+                const uint64_t y = (uint64_t)__shfl_up((unsigned long long)c, d);
+                if (lane >= d) c += y;
+            }
+            if (lane < kPlanBlock / 64) wt[lane].a = c - w;  // exclusive prefix of wave `lane`
+            if (lane == kPlanBlock / 64 - 1) wt[kPlanBlock / 64].b = c;
+        }
+        __syncthreads();
+        const SFun r{0u, 0u, wt[wave].a + v};
+        total = SFun{0u, 0u, wt[kPlanBlock / 64].b};
+        __syncthreads();
+        return r;
+    }
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const SFun y = sf_shfl_up(x, d);
@@ -261,12 +295,16 @@ __global__ void __launch_bounds__(kPlanBlock) plan_count_kernel(const uint64_t* 
     const uint64_t i = (uint64_t)eb * kPlanBlock + threadIdx.x;
     uint32_t full = 0u, mine = 0u;
     bool ok = true;  // length within the band of the reference (PlanRun::in_band)
+    uint64_t oi = 0u;
+    uint32_t li = 0u;
     if (i < n) {
         const uint32_t l = lengths[i];
+        li = l;
         ok = PlanRun::in_band(l, ref);
-        if (!is_small(l, pg)) {  // offsets are read only for the plan's own entries
-            mine = 1u;
-            const EntryPlan p = plan_entry(offsets[i], l, size, pg);
+        if (!is_small(l, pg)) {  // offsets are read only for the plan's own entries (all of them when
+            mine = 1u;           // the stream route is possible: it has no short class)
+            oi = offsets[i];
+            const EntryPlan p = plan_entry(oi, l, size, pg);
             if (p.kind == 0) {
                 if (p.jh != pg.jc) atomicAdd(&col[p.jh], 1u);
                 full = p.full;
@@ -296,7 +334,7 @@ __global__ void __launch_bounds__(kPlanBlock) plan_count_kernel(const uint64_t* 
         SEnt e;
         bool sh, jp;
         uint64_t J1;
-        const SFun el = stream_elem(offsets, lengths, i, n, size, sa.mis, e, sh, jp, J1);
+        const SFun el = stream_elem(offsets, lengths, i, n, size, sa.mis, oi, li, e, sh, jp, J1);
         SFun tot;
         (void)block_scan_sf(el, swt, tot);  // (its barriers also order sjumps' reset)
         const uint32_t nj = (uint32_t)__popcll(__ballot(e.in && jp));
@@ -442,15 +480,16 @@ __global__ void __launch_bounds__(kPlanBlock, BKD_PLAN_OCC) plan_emit_kernel(con
             SEnt e;
             bool sh, jp;
             uint64_t J1;
-            const SFun el = stream_elem(offsets, lengths, i, n, size, sa.mis, e, sh, jp, J1);
+            const uint64_t o = i < n ? offsets[i] : 0u;
+            const uint32_t l = i < n ? lengths[i] : 0u;
+            const SFun el = stream_elem(offsets, lengths, i, n, size, sa.mis, o, l, e, sh, jp, J1);
             SFun tot;
             const SFun inc = block_scan_sf(el, swt, tot);
             const uint64_t V = sf_apply(inc, sa.sbase[eb]) - J1;  // its first new line
             const uint64_t P0 = V - (sh ? 1u : 0u);                 // its first line
             if (rep == 0u && i < n) {
-                const uint64_t o = offsets[i];
                 sa.spos[i] = e.in ? P0 : (1ull << 63);
-                sa.srec[i] = u32x4{(uint32_t)o, (uint32_t)(o >> 32), lengths[i], seeds ? seeds[i] : seed_all};
+                sa.srec[i] = u32x4{(uint32_t)o, (uint32_t)(o >> 32), l, seeds ? seeds[i] : seed_all};
             }
             uint32_t cnt = 0u;
             uint64_t tf0 = 0u;
@@ -709,7 +748,8 @@ __global__ void __launch_bounds__(1024, BKD_PLAN_OCC) plan_combine_kernel(
         // the stream route (xtab = x^(8 * 4096), one tile): an entry whose lines span tiles t0 < t1
         // is plast[t0], pfirst[t0 + 1 .. t1 - 1] (whole tiles) joined by Horner with X, then
         // * x^(1024 L) ^ pfirst[t1] (its last L lines), then * x^(-8 pad). Entries outside the
-        // stream (empty, a padded message under 4 bytes, out of range) are done here one thread each.
+        // stream (empty, a padded message under 4 bytes, out of range) are done here one thread each;
+        // an entry inside one tile has its raw register in out[i] (pad product and inversion here).
         auto piece = [&](uint64_t t0, uint64_t t1, uint32_t m, uint32_t c) -> uint32_t {  // weight X^c
             return c + 1u == m ? sa.plast[t0] : sa.pfirst[t1 - 1u - c];
         };
@@ -740,7 +780,12 @@ __global__ void __launch_bounds__(1024, BKD_PLAN_OCC) plan_combine_kernel(
                     if (m > kCombineSerial) {
                         is_big = 1u;
                         if (reps == 1u) big[atomicAdd(&nbig, 1u)] = (uint32_t)threadIdx.x;
-                    } else if (m && rep == 0u) {
+                    } else if (m == 0u) {  // inside one tile: the tile kernel left its raw register
+                        if (rep == 0u) {
+                            const uint32_t reg = out[i];
+                            out[i] = ~(e.pad ? gf_mul_bits(xinv[e.pad], reg, poly) : reg);
+                        }
+                    } else if (rep == 0u) {
                         uint32_t reg = piece(t0, t1, (uint32_t)m, (uint32_t)m - 1u);
                         for (int c0 = (int)m - 2; c0 >= 0; c0 -= 8) {
                             uint32_t pv[8];

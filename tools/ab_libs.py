@@ -36,6 +36,8 @@ def main(paths):
                 getattr(L, fn).argtypes = args
         if os.environ.get("AB_SMALL") and hasattr(L, "bkd_set_plan_small"):
             L.bkd_set_plan_small(int(os.environ["AB_SMALL"]))
+        if os.environ.get("AB_MODE") and hasattr(L, "bkd_set_plan_mode"):  # 0 auto, 1 direct, 2 plan, 3 stream
+            L.bkd_set_plan_mode(int(os.environ["AB_MODE"]))
         if os.environ.get("AB_GEOM"):  # lanes,steps,merge for the plan (bkd_set_plan_geometry)
             assert L.bkd_set_plan_geometry(*(int(v) for v in os.environ["AB_GEOM"].split(","))) == 0
         libs[os.path.basename(p)] = L
