@@ -388,6 +388,11 @@ def set_plan_mode(mode: int) -> None:
     check(lib().bkd_set_plan_mode(mode))
 
 
+def set_stream_range_max(lines: int) -> None:
+    """Stream route: lines per range above which every entry is taken whole (default 2^22)."""
+    check(lib().bkd_set_stream_range_max(lines))
+
+
 def set_plan_small(max_bytes: int = 192) -> None:
     """Entries of <= max_bytes of a planned indexed batch run in the short-entry launch (0 = none)."""
     check(lib().bkd_set_plan_small(max_bytes))

@@ -25,6 +25,7 @@
 #include "../../include/bkdigest.h"
 #include "crc_kernels.hpp"
 #include "plan_kernels.hpp"
+#include "stream_kernels.hpp"
 #include "crc_tables.hpp"
 #include "host_batch.hpp"
 #include "host_crc.hpp"
@@ -73,8 +74,20 @@ struct StreamScratch {
     // PlanRun word of the plans enqueued on this stream and the epoch of the latest one
     uint32_t* run = nullptr;
     uint32_t* uni = nullptr;  // PlanRun uniform-lengths word (the epoch of the call it holds for)
-    uint32_t* sword = nullptr;  // stream-route word (StreamArgs::word: the epoch of the call that takes it)
+    uint32_t* ticket = nullptr;  // the stream route's entry-block ticket (StreamArgs::ticket), 0 between calls
     uint32_t epoch = 0;
+    hipError_t ticket_word(hipStream_t st, uint32_t** out) {
+        if (!ticket) {
+            hipError_t e = hipMalloc((void**)&ticket, sizeof(uint32_t));
+            if (e == hipSuccess) e = hipMemsetAsync(ticket, 0, sizeof(uint32_t), st);
+            if (e != hipSuccess) {
+                ticket = nullptr;
+                return e;
+            }
+        }
+        *out = ticket;
+        return hipSuccess;
+    }
     // verify gate word (verify_gate_kernel) and the epoch of the latest verify on this stream
     uint32_t* vflag = nullptr;
     uint32_t vepoch = 0;
@@ -112,18 +125,6 @@ struct StreamScratch {
             }
         }
         *out = uni;
-        return hipSuccess;
-    }
-    hipError_t stream_word(hipStream_t st, uint32_t** out) {
-        if (!sword) {
-            hipError_t e = hipMalloc((void**)&sword, sizeof(uint32_t));
-            if (e == hipSuccess) e = hipMemsetAsync(sword, 0, sizeof(uint32_t), st);
-            if (e != hipSuccess) {
-                sword = nullptr;
-                return e;
-            }
-        }
-        *out = sword;
         return hipSuccess;
     }
     hipError_t flag(hipStream_t st, uint32_t** out) {
@@ -182,7 +183,6 @@ struct DeviceState {
     int cus = 0;
     uint32_t* tables[2][kNumLaneChoices] = {};  // [algo][lane choice] compact operator images
     uint32_t* xinv[2] = {};       // [algo] x^(-8k), k = 0..127: removes the plan's zero padding
-    uint32_t* xline[2] = {};      // [algo] x^(1024 L), L = 0..32: the stream route's last piece of L lines
     std::shared_mutex maps_mu;    // guards xtab and scratch
     std::map<uint64_t, uint32_t*> xtab;  // (algo, CH) -> x^(8*CH) operator for the plan's combine
     std::map<hipStream_t, std::unique_ptr<StreamScratch>> scratch;
@@ -191,6 +191,7 @@ struct DeviceState {
 std::mutex g_mu;  // device initialisation only
 DeviceState g_dev[kMaxDevices];
 std::atomic<int> g_forced_lanes{0};
+std::atomic<uint64_t> g_stream_max_tl{1ull << 22};  // bkd_set_stream_range_max (StreamArgs::maxtl)
 std::atomic<int> g_plan_mode{0};  // 0 auto, 1 direct (one entry per group), 2 chunked plan, 3 stream route
 
 // Chunked plan geometry (bkd_set_plan_geometry): lanes per group, steps per full chunk
@@ -282,10 +283,6 @@ int init_device_locked(int dev) {
         for (uint32_t k = 0; k < 128; ++k) inv[k] = bkd::gf2::xpow_neg8(algo, k);
         BKD_HIP(hipMalloc(&ds.xinv[algo], sizeof(inv)));
         BKD_HIP(hipMemcpy(ds.xinv[algo], inv, sizeof(inv), hipMemcpyHostToDevice));
-        uint32_t xl[bkd::kTileLines + 1];
-        for (uint32_t k = 0; k <= bkd::kTileLines; ++k) xl[k] = bkd::gf2::xpow(algo, 1024ull * k);
-        BKD_HIP(hipMalloc(&ds.xline[algo], sizeof(xl)));
-        BKD_HIP(hipMemcpy(ds.xline[algo], xl, sizeof(xl), hipMemcpyHostToDevice));
     }
     BKD_HIP(hipSetDevice(prev));
     ds.ready.store(true, std::memory_order_release);
@@ -411,17 +408,67 @@ template <int G>
 void launch_plan_chunks(const bkd::PlanRun& run, const uint8_t* base, const bkd::PlanDesc* descs,
                         const uint32_t* count, const uint32_t* tab,
                         uint32_t* out, uint32_t* partials, const bkd::PlanDirectSrc& ov, int blocks, hipStream_t st,
-                        uint32_t* err, int pf, const bkd::StreamArgs& sa, const uint32_t* xinv, uint32_t poly) {
+                        uint32_t* err, int pf) {
     // pf: read once by launch_plan (one value per call)
     if (pf == 8)
         hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 8, kNT, bkd::PlanDirectSrc>), dim3((unsigned)blocks),
-                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err, sa, xinv, poly);
+                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err);
     else if (pf == 4)
         hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 4, kNT, bkd::PlanDirectSrc>), dim3((unsigned)blocks),
-                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err, sa, xinv, poly);
+                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err);
     else
         hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 2, kNT, bkd::PlanDirectSrc>), dim3((unsigned)blocks),
-                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err, sa, xinv, poly);
+                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err);
+}
+
+// Indexed batch through the stream route (stream_kernels.hpp): positions (one launch, decoupled
+// look-back), the range kernel, the combine; stream-ordered, no host sync.
+int launch_stream(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, const uint64_t* offsets,
+                  const uint32_t* lengths, uint64_t n, const uint32_t* seeds, uint32_t seed_all, uint32_t* out,
+                  hipStream_t st, uint32_t mis) {
+    const uint32_t nb = (uint32_t)((n + bkd::kPlanBlock - 1) / bkd::kPlanBlock);
+    const uint32_t ngroups = (uint32_t)ds.cus * (uint32_t)(bkd::kBlock / 8);
+    Carver cv;
+    const size_t o_desc = cv.take((size_t)nb * 8), o_hdr = cv.take(64), o_pos = cv.take((size_t)n * 8),
+                 o_rec = cv.take((size_t)n * 16), o_pf = cv.take((size_t)ngroups * 4),
+                 o_pl = cv.take((size_t)ngroups * 4);
+    StreamScratch& sc = scratch_for(ds, st);
+    std::lock_guard<std::recursive_mutex> lk(sc.mu);
+    uint8_t* sb = nullptr;
+    uint32_t* err = nullptr;
+    uint32_t* ticket = nullptr;
+    hipError_t e = sc.get(0, cv.used, st, &sb);
+    if (e == hipSuccess) e = sc.flag(st, &err);
+    if (e == hipSuccess) e = sc.ticket_word(st, &ticket);
+    if (e != hipSuccess) return fail(BKD_ERR_NOMEM, std::string("stream scratch: ") + hipGetErrorString(e));
+    if (++sc.epoch == 0u) ++sc.epoch;
+    bkd::StreamArgs sa{};
+    sa.sdesc = Carver::at<uint64_t>(sb, o_desc);
+    sa.shdr = Carver::at<uint64_t>(sb, o_hdr);
+    sa.spos = Carver::at<uint64_t>(sb, o_pos);
+    sa.srec = Carver::at<bkd::u32x4>(sb, o_rec);
+    sa.pfirst = Carver::at<uint32_t>(sb, o_pf);
+    sa.plast = Carver::at<uint32_t>(sb, o_pl);
+    sa.ticket = ticket;
+    sa.ngroups = ngroups;
+    sa.mis = mis;
+    sa.epoch = sc.epoch;
+    sa.maxtl = g_stream_max_tl.load();
+    const uint32_t* tab = ds.tables[algo][lane_index(8)];
+    const uint32_t* btab = tab + bkd::gf2::byte_table_offset(8);
+    hipLaunchKernelGGL(bkd::plan_stream_kernel, dim3(nb), dim3(bkd::kPlanBlock), 0, st, offsets, lengths, seeds, seed_all,
+                       size, n, nb, sa);
+    hipLaunchKernelGGL((bkd::crc_stream_ranges_kernel<kNT>), dim3(ds.cus), dim3(bkd::kBlock), 0, st, base, size, offsets,
+                       lengths, seeds, seed_all, n, tab, out, err, sa);
+#ifndef BKD_PLAN_GRID
+#define BKD_PLAN_GRID 2
+#endif
+    const uint32_t cgrid = std::min<uint32_t>(nb, (uint32_t)BKD_PLAN_GRID * (uint32_t)ds.cus);
+    hipLaunchKernelGGL(bkd::stream_combine_kernel, dim3(cgrid), dim3(1024), 0, st, base, offsets, lengths, seeds, seed_all,
+                       size, n, nb, btab, ds.xinv[algo], bkd::gf2::poly(algo), bkd::gf2::xpow(algo, 1024), sa, out, err);
+    e = hipGetLastError();
+    if (e != hipSuccess) return fail(BKD_ERR_HIP, std::string("stream kernels: ") + hipGetErrorString(e));
+    return BKD_OK;
 }
 
 // Indexed batch through the chunked plan (plan_kernels.hpp): five stream-ordered kernels, no
@@ -467,24 +514,18 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     const uint64_t capacity = std::min<uint64_t>(n + (size + 128u * n) / pg.ch + 16, 0xFFFFFFF0ull);
     const uint32_t nb = (uint32_t)((n + bkd::kPlanBlock - 1) / bkd::kPlanBlock);
     const uint32_t ncols = bkd::plan_ncols(pg);
-    // The stream route: tiles of 32 lines of 8-lane steps, joined with x^(8 * 4096) —
-    // the plan's own operator at its default geometry. Decided on the device by plan_scan (at most
-    // jumps_max entries that do not continue their predecessor's lines; forced: any number).
-    // (the tile kernel numbers lines, tiles and entries in 32 bits)
-    const bool stream = BKD_STREAM && (mode == 0 || mode == 3) && G == 8 && pg.ch == 4096u && pg.small == 0u &&
-                        size < (1ull << 38) && n < (1ull << 30);
-    // tiles: non-overlapping entries span at most size / 128 + 2 n lines, each jump wastes < 1 tile
-    const uint64_t tcap = stream ? (size / 128u + 2u * n) / bkd::kTileLines + n + 16u : 0u;
+    // The stream route (stream_kernels.hpp): every ragged batch without a short class
+    // at the default geometry (8-lane groups; the tile kernel numbers device lines and entries in
+    // 32 bits); any index order, gaps or overlaps. Mode 2 keeps the chunked plan.
+    if (BKD_STREAM && (mode == 0 || mode == 3) && G == 8 && pg.small == 0u && size < (1ull << 38) &&
+        n < (1ull << 30) && !ext_flag)
+        return launch_stream(ds, algo, base, size, offsets, lengths, n, seeds, seed_all, out, st, pg.mis);
     Carver cv;
     const size_t o_blk = cv.take((size_t)nb * ncols * 4), o_live = cv.take((size_t)nb * 4),
                  o_bok = cv.take((size_t)nb * 4),
                  o_blkoff = cv.take((size_t)nb * ncols * 4), o_hdr = cv.take(bkd::kHdrWords * 4),
                  o_ps = cv.take((size_t)n * 4), o_hs = cv.take((size_t)n * 4), o_part = cv.take((size_t)capacity * 4),
                  o_desc = cv.take((size_t)capacity * sizeof(bkd::PlanDesc));
-    const size_t o_sblk = cv.take(stream ? (size_t)nb * 24 : 0), o_sbase = cv.take(stream ? (size_t)nb * 8 : 0),
-                 o_shdr = cv.take(stream ? 32 : 0), o_spos = cv.take(stream ? (size_t)n * 8 : 0),
-                 o_srec = cv.take(stream ? (size_t)n * 16 : 0), o_tf = cv.take((size_t)tcap * 4),
-                 o_tk = cv.take((size_t)tcap * 4), o_pf = cv.take((size_t)tcap * 4), o_pl = cv.take((size_t)tcap * 4);
     StreamScratch& sc = scratch_for(ds, st);
     std::lock_guard<std::recursive_mutex> lk(sc.mu);
     uint8_t* sb = nullptr;
@@ -503,28 +544,9 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     if (e == hipSuccess) e = sc.flag(st, &err);
     if (e == hipSuccess && pg.small) e = sc.run_word(st, &run_word);
     if (e == hipSuccess && gate) e = sc.uni_word(st, &uni);
-    uint32_t* sword = nullptr;
-    if (e == hipSuccess && stream) e = sc.stream_word(st, &sword);
     if (e != hipSuccess) return fail(BKD_ERR_NOMEM, std::string("plan scratch: ") + hipGetErrorString(e));
     if (++sc.epoch == 0u) ++sc.epoch;  // 0 is the words' initial value
     const bkd::PlanRun run = ext_flag ? bkd::PlanRun{ext_flag, nullptr, ext_epoch} : bkd::PlanRun{run_word, uni, sc.epoch};
-    bkd::StreamArgs sa{};
-    if (stream) {
-        sa.sblk = Carver::at<uint64_t>(sb, o_sblk);
-        sa.sbase = Carver::at<uint64_t>(sb, o_sbase);
-        sa.shdr = Carver::at<uint64_t>(sb, o_shdr);
-        sa.spos = Carver::at<uint64_t>(sb, o_spos);
-        sa.srec = Carver::at<bkd::u32x4>(sb, o_srec);
-        sa.tfirst = Carver::at<uint32_t>(sb, o_tf);
-        sa.tk0 = Carver::at<uint32_t>(sb, o_tk);
-        sa.pfirst = Carver::at<uint32_t>(sb, o_pf);
-        sa.plast = Carver::at<uint32_t>(sb, o_pl);
-        sa.cap = tcap;
-        sa.jumps_max = mode == 3 ? UINT64_MAX : n / 64u + 1u;
-        sa.mis = pg.mis;
-        sa.word = sword;
-        sa.epoch = sc.epoch;
-    }
     uint32_t *blk = Carver::at<uint32_t>(sb, o_blk), *blive = Carver::at<uint32_t>(sb, o_live),
              *bok = gate ? Carver::at<uint32_t>(sb, o_bok) : nullptr,
              *blkoff = Carver::at<uint32_t>(sb, o_blkoff), *hdr = Carver::at<uint32_t>(sb, o_hdr),
@@ -545,30 +567,26 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
 #endif
     const uint32_t pgrid = BKD_PLAN_GRID ? (uint32_t)BKD_PLAN_GRID * (uint32_t)ds.cus : 0xFFFFFFFFu;
     hipLaunchKernelGGL(bkd::plan_count_kernel, dim3(std::min(nb, pgrid)), dim3(bkd::kPlanBlock), 0, st, offsets,
-                       lengths, size, n, pg, blk, blive, nb, run, bok, sa);
-    hipLaunchKernelGGL(bkd::plan_scan_kernel, dim3(ncols + (gate ? 1u : 0u) + (stream ? 1u : 0u)),
-                       dim3(bkd::kPlanBlock), 0, st, blk, nb, blkoff, hdr, run, ncols, bok, sa);
+                       lengths, size, n, pg, blk, blive, nb, run, bok);
+    hipLaunchKernelGGL(bkd::plan_scan_kernel, dim3(ncols + (gate ? 1u : 0u)), dim3(bkd::kPlanBlock), 0, st, blk, nb,
+                       blkoff, hdr, run, ncols, bok);
     // few entry blocks (large entries): replicate emit and combine blocks so ~2 blocks per CU work
     const uint32_t reps = nb >= 2u * (uint32_t)ds.cus ? 1u : std::min<uint32_t>(64u, (2u * (uint32_t)ds.cus + nb - 1u) / nb);
     hipLaunchKernelGGL(bkd::plan_emit_kernel, dim3(std::min(nb * reps, pgrid)), dim3(bkd::kPlanBlock), 0, st, offsets,
-                       lengths, seeds, seed_all, size, n, pg, capacity, blkoff, pslot, hslot, hdr, descs, reps, blive, nb, run,
-                       sa);
+                       lengths, seeds, seed_all, size, n, pg, capacity, blkoff, pslot, hslot, hdr, descs, reps, blive, nb, run);
     const uint32_t* tab = ds.tables[algo][lane_index(G)];
     const bkd::PlanDirectSrc ov{n, offsets, lengths, seeds, seed_all, size, out, pslot, hdr, capacity, false};
     switch (G) {
-        case 4: launch_plan_chunks<4>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf, sa, ds.xinv[algo], bkd::gf2::poly(algo)); break;
-        case 8: launch_plan_chunks<8>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf, sa, ds.xinv[algo], bkd::gf2::poly(algo)); break;
-        case 16: launch_plan_chunks<16>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf, sa, ds.xinv[algo], bkd::gf2::poly(algo)); break;
-        case 32: launch_plan_chunks<32>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf, sa, ds.xinv[algo], bkd::gf2::poly(algo)); break;
-        default: launch_plan_chunks<64>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf, sa, ds.xinv[algo], bkd::gf2::poly(algo)); break;
+        case 4: launch_plan_chunks<4>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
+        case 8: launch_plan_chunks<8>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
+        case 16: launch_plan_chunks<16>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
+        case 32: launch_plan_chunks<32>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
+        default: launch_plan_chunks<64>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
     }
-    if (stream)
-        hipLaunchKernelGGL((bkd::crc_stream_tiles_kernel<kNT>), dim3(ds.cus), dim3(bkd::kBlock), 0, st, base, size, n,
-                           tab, out, run, sa, ds.xinv[algo], bkd::gf2::poly(algo));
     const uint32_t* btab = tab + bkd::gf2::byte_table_offset(G);
     hipLaunchKernelGGL(bkd::plan_combine_kernel, dim3(std::min(nb * reps, pgrid)), dim3(1024), 0, st, base, offsets, lengths, seeds,
                        seed_all, size, n, pg, xtab, bkd::gf2::xpow(algo, 8ull * pg.ch), btab, ds.xinv[algo],
-                       bkd::gf2::poly(algo), pslot, hslot, partials, out, err, reps, blive, nb, run, sa, ds.xline[algo]);
+                       bkd::gf2::poly(algo), pslot, hslot, partials, out, err, reps, blive, nb, run);
     e = hipGetLastError();
     if (e != hipSuccess) return fail(BKD_ERR_HIP, std::string("plan kernels: ") + hipGetErrorString(e));
     return BKD_OK;
@@ -1249,6 +1267,12 @@ int bkd_init(int device) {
 
 const char* bkd_last_error(void) { return t_err.c_str(); }
 
+int bkd_set_stream_range_max(uint64_t lines) {
+    if (lines < 4u) return fail(BKD_ERR_INVALID_ARG, "stream range bound must be at least 4 lines");
+    g_stream_max_tl.store(lines);
+    return BKD_OK;
+}
+
 int bkd_set_fold_schedule(int schedule) {
     if (schedule < 0 || schedule > 2) return fail(BKD_ERR_INVALID_ARG, "fold schedule must be 0, 1 or 2");
     g_fold_sched.store(schedule);
@@ -1401,7 +1425,7 @@ int bkd_stream_release(void* stream) {
         BKD_HIP(hipStreamSynchronize(st));  // the stream's own work is done with them
         for (int k = 0; k < 3; ++k)
             if (sc->buf[k]) BKD_HIP(hipFree(sc->buf[k]));
-        for (uint32_t* w : {sc->err, sc->run, sc->uni, sc->vflag, sc->sword})
+        for (uint32_t* w : {sc->err, sc->run, sc->uni, sc->vflag, sc->ticket})
             if (w) BKD_HIP(hipFree(w));
         if (sc->h_err) BKD_HIP(hipHostFree(sc->h_err));
     }

@@ -1324,293 +1324,6 @@ __device__ __forceinline__ void plan_chunks_loop(const uint32_t* lds, uint32_t l
 }
 
 
-// a * b mod P, bitwise (no tables): 32 shift/xor steps, for the few products per entry that have
-// no operator table (x^(-8*pad), powers of X).
-__device__ __forceinline__ uint32_t gf_mul_bits(uint32_t a, uint32_t b, uint32_t poly) {
-    uint32_t prod = 0u, cur = b;
-#pragma unroll
-    for (int k = 31; k >= 0; --k) {
-        prod ^= ((a >> k) & 1u) ? cur : 0u;
-        cur = (cur >> 1) ^ ((cur & 1u) ? poly : 0u);
-    }
-    return prod;
-}
-
-__device__ __forceinline__ uint32_t gf_pow_bits(uint32_t x, uint32_t e, uint32_t poly) {
-    uint32_t r = 0x80000000u;  // x^0
-    while (e) {
-        if (e & 1u) r = gf_mul_bits(r, x, poly);
-        x = gf_mul_bits(x, x, poly);
-        e >>= 1;
-    }
-    return r;
-}
-
-// ---- the stream route for ragged batches (DESIGN.md §3 "stream route"; CPU model of the same
-// decomposition: tests/stream_model.py, checked against the oracle on every index layout) ----
-// The entries' 128-byte device lines are laid end to end in index order — a line that holds one
-// entry's end and the next entry's start counted once — and cut into tiles of kTileLines lines
-// (an entry that does not continue its predecessor's lines starts a new tile, so a tile's lines are
-// consecutive device lines). One 8-lane group folds one tile line by line: each line is loaded once
-// and folded into every entry it holds, the bytes outside the entry zeroed in the very register
-// that is folded (no byte outside an entry can change its digest). An entry that lies inside one
-// tile gets its digest there; a longer entry leaves one raw register per tile (pfirst / plast) and
-// plan_combine joins them, x^(1024 L) per piece of L lines, then x^(-8 pad).
-constexpr uint32_t kTileLines = 32;  // 4 KiB per 8-lane group
-#ifndef BKD_STREAM
-#define BKD_STREAM 1  // 0: the stream route is not built (indexed batches take the chunked plan)
-#endif
-
-struct StreamArgs {
-    uint64_t* sblk;      // [3 nb] per entry block: its position function (f << 63 | a, b) and its jumps
-    uint64_t* sbase;     // [nb] stream position at the start of each entry block
-    uint64_t* shdr;      // [0] end position, [1] tiles, [2] jumps
-    uint64_t* spos;      // [n] position of entry i's first line (bit 63: not in the stream)
-    u32x4* srec;         // [n] {offset lo, offset hi, length, seed} of entry i
-    uint32_t* tfirst;    // [cap] entry holding the tile's first line
-    uint32_t* tk0;       // [cap] that line's index within the entry
-    uint32_t* pfirst;    // [cap] raw register of the tile's first piece (its entry began before the tile)
-    uint32_t* plast;     // [cap] raw register of the tile's last piece (its entry goes on past the tile)
-    uint64_t cap;        // tile capacity
-    uint64_t jumps_max;  // the stream route is taken with at most this many jumps
-    uint32_t mis;        // device address of base modulo 128
-    uint32_t* word;      // route word: `epoch` when the stream route is taken (plan_scan decides)
-    uint32_t epoch;
-    __device__ __forceinline__ bool on() const { return word && *word == epoch; }
-};
-
-// Stream geometry of one entry (stream_model.Geo).
-struct SEnt {
-    uint64_t as, ae;  // mis + offset, mis + offset + length
-    uint64_t F, Lst;  // first and last 128-byte line
-    uint32_t d, pad;  // bytes of its first line before the entry; bytes of its last line after it
-    bool in;          // in the stream: valid, non-empty, padded message of >= 4 bytes (the seed image)
-};
-
-__device__ __forceinline__ SEnt stream_ent(uint64_t o, uint32_t l, uint64_t size, uint32_t mis) {
-    SEnt e;
-    e.as = (uint64_t)mis + o;
-    e.ae = e.as + l;
-    e.F = e.as >> 7;
-    e.Lst = l ? (e.ae - 1u) >> 7 : e.F;
-    e.d = (uint32_t)(e.as & 127u);
-    e.pad = (128u - (uint32_t)(e.ae & 127u)) & 127u;
-    e.in = !(o > size || (uint64_t)l > size - o) && l != 0u && l + e.pad >= 4u;
-    return e;
-}
-
-// shared: e's first line is p's last line (counted once); jump: e starts a new tile
-__device__ __forceinline__ void stream_link(const SEnt& p, const SEnt& e, bool& shared, bool& jump) {
-    shared = p.in && e.F == p.Lst;
-    jump = !(p.in && (e.F == p.Lst || e.F == p.Lst + 1u));
-}
-
-// Keeps bytes [a, b) of a 16-byte block (block coordinates, any range), zeroes the rest.
-__device__ __forceinline__ u32x4 keep_range(u32x4 w, int32_t a, int32_t b) {
-    auto m = [](uint32_t x, int32_t lo, int32_t hi) -> uint32_t {  // (selects, no branches)
-        const int32_t a = lo < 0 ? 0 : lo, b = hi > 4 ? 4 : hi, wd = b - a;
-        const uint32_t msk = (0xFFFFFFFFu >> ((uint32_t)(32 - 8 * wd) & 31u)) << ((uint32_t)(8 * a) & 31u);
-        return wd > 0 ? x & msk : 0u;
-    };
-    w.x = m(w.x, a, b);
-    w.y = m(w.y, a - 4, b - 4);
-    w.z = m(w.z, a - 8, b - 8);
-    w.w = m(w.w, a - 12, b - 12);
-    return w;
-}
-
-// Geometry of an entry relative to a tile's first line L0 (byte 0 = the first byte of line L0),
-// in 32-bit registers: byte positions clamped to +-2^30, lines to +-2^23 (an entry that far from
-// the tile never meets its lines).
-struct SRel {
-    int32_t a, e;    // first byte and end
-    int32_t sF, sL;  // first and last line (steps of the tile)
-    uint32_t d, pad;
-    bool in;
-};
-
-__device__ __forceinline__ SRel srel(const u32x4& r, uint64_t L0, uint64_t size, uint32_t mis) {
-    const uint64_t o = (uint64_t)r.x | ((uint64_t)r.y << 32);
-    const uint32_t l = r.z;
-    SRel q;
-    const int64_t A = (int64_t)((uint64_t)mis + o) - (int64_t)(L0 << 7), E = A + (int64_t)l;
-    auto cl = [](int64_t v, int64_t m) -> int32_t { return (int32_t)(v < -m ? -m : (v > m ? m : v)); };
-    q.a = cl(A, 1 << 30);
-    q.e = cl(E, 1 << 30);
-    q.sF = cl(A >> 7, 1 << 23);
-    q.sL = cl((E - 1) >> 7, 1 << 23);
-    q.d = (uint32_t)A & 127u;
-    q.pad = (128u - ((uint32_t)E & 127u)) & 127u;
-    q.in = !(o > size || (uint64_t)l > size - o) && l != 0u && l + q.pad >= 4u;
-    return q;
-}
-
-// The tiles of the stream in grid stride, one per 8-lane group per round of kTileLines steps; four
-// register sets hold the next four lines (the last steps of a round load the next tile's first
-// lines). Every load is unconditional, at a fixed point of the round, so that the compiler's memory
-// waits stay counted (no drain of the lines in flight): the next tile's index words and first
-// record one round ahead, and beside every line a window of the eight records after the current
-// entry, one per lane (`W`, base index `B`), used four steps later like the line itself: an entry
-// change takes its record from the window with a group shuffle. Only when more than eight entries
-// began within five lines (entries of under half a line) is a record loaded on the spot, on a path
-// that waits for itself. A record loaded one step ahead instead made every entry change wait for
-// it and for the three lines before it: mixed 1 KiB entries 2x slower, Zipf 2.4x (profiles/r04c_*).
-// The loop body is the four steps of one line set, so the hot loop stays small in the instruction
-// cache. An entry's digest leaves here raw; plan_combine applies x^(-8 pad) and the inversion.
-template <bool NT>
-__device__ __forceinline__ void stream_tiles_loop(const uint32_t* lds, uint32_t lanereg, int g,
-                                                  const uint8_t* __restrict__ base, uint64_t size,
-                                                  const StreamArgs& sa, uint64_t n, uint64_t gid, uint64_t ngroups,
-                                                  uint32_t* __restrict__ out) {
-    constexpr uint32_t TL = kTileLines;
-    // line and tile numbers fit 32 bits (launch_plan takes the stream route below 2^38 bytes)
-    const uint32_t end = (uint32_t)sa.shdr[0], ntiles = (uint32_t)sa.shdr[1];
-    if (ntiles == 0u || size == 0u) return;  // (kernel-uniform)
-    const uint8_t* lb = base - sa.mis;  // device line 0 (the line holding base)
-    const uint32_t lmax = (uint32_t)(((uint64_t)sa.mis + size - 1u) >> 7);
-    const uint32_t mis = sa.mis;
-    auto ld_line = [&](uint32_t L) { return ld16<NT>(lb + ((uint64_t)(L < lmax ? L : lmax) << 7) + 16 * g); };
-    auto ld_rec = [&](uint64_t i) { return sa.srec[i < n ? i : n - 1u]; };
-    auto first_line = [&](const u32x4& r, uint32_t k) -> uint32_t {
-        return (uint32_t)(((uint64_t)mis + ((uint64_t)r.x | ((uint64_t)r.y << 32))) >> 7) + k;
-    };
-    auto clampt = [&](uint32_t t) { return t < ntiles ? t : ntiles - 1u; };
-    auto lines_of = [&](uint32_t t) -> uint32_t { return t < ntiles ? (end - t * TL < TL ? end - t * TL : TL) : 1u; };
-    const uint32_t ng = (uint32_t)ngroups;
-
-    // this round's tile (t, tf, k0) and the next round's (t1, tf1, k01); RA: the first record of
-    // this tile at a round's start, of the next tile from then on
-    uint32_t t = (uint32_t)gid;
-    uint32_t tf = sa.tfirst[clampt(t)], k0 = sa.tk0[clampt(t)];
-    u32x4 RA = ld_rec(tf);
-    // record windows: lane g of the group holds record B + g
-    uint32_t B0 = tf + 1u, B1 = B0, B2 = B0, B3 = B0;
-    const int lane8 = (int)(threadIdx.x & 56u);  // the group's first lane in its wave
-    u32x4 W0 = ld_rec((uint64_t)B0 + g), W1 = ld_rec((uint64_t)B0 + g), W2 = ld_rec((uint64_t)B0 + g),
-          W3 = ld_rec((uint64_t)B0 + g);
-    uint32_t t1 = t + ng;
-    uint32_t tf1 = sa.tfirst[clampt(t1)], k01 = sa.tk0[clampt(t1)];
-    uint32_t L0 = first_line(RA, k0);
-    uint32_t nl = lines_of(t);
-    u32x4 X0 = ld_line(L0), X1 = ld_line(L0 + (1u < nl ? 1u : nl - 1u)), X2 = ld_line(L0 + (2u < nl ? 2u : nl - 1u)),
-          X3 = ld_line(L0 + (3u < nl ? 3u : nl - 1u));
-
-#define BKD_STREAM_STEP(XS, WS, BS, S)                                                                \
-    {                                                                                                 \
-        const uint32_t s_ = (S);                                                                      \
-        const u32x4 w = XS;                                                                           \
-        bool more = live && s_ < nla;                                                                 \
-        while (__any(more)) {                                                                         \
-            if (more) {                                                                               \
-                const int32_t sv = (int32_t)s_;                                                       \
-                const int32_t lbase = 128 * sv + 16 * g;                                              \
-                u32x4 wm = w;                                                                         \
-                if (sv == e.sF || sv == e.sL) wm = keep_range(w, e.a - lbase, e.e - lbase);           \
-                if (sv == e.sF) {                                                                     \
-                    const int64_t dd = (int64_t)e.d - 16 * g;                                         \
-                    wm.x ^= place_seed(r0, dd);                                                       \
-                    wm.y ^= place_seed(r0, dd - 4);                                                   \
-                    wm.z ^= place_seed(r0, dd - 8);                                                   \
-                    wm.w ^= place_seed(r0, dd - 12);                                                  \
-                }                                                                                     \
-                if (sv == e.sF + 1 && e.d > 124u && g == 0) wm.x ^= place_seed(r0, (int64_t)e.d - 128); \
-                const uint32_t m0 = mul_main_add(lds, c0, lanereg, wm.x);                             \
-                const uint32_t m1 = mul_main_add(lds, c1, lanereg, wm.y);                             \
-                const uint32_t m2 = mul_main_add(lds, c2, lanereg, wm.z);                             \
-                const uint32_t m3 = mul_main_add(lds, c3, lanereg, wm.w);                             \
-                c0 = fresh ? wm.x : m0;                                                               \
-                c1 = fresh ? wm.y : m1;                                                               \
-                c2 = fresh ? wm.z : m2;                                                               \
-                c3 = fresh ? wm.w : m3;                                                               \
-                fresh = false;                                                                        \
-                more = false;                                                                         \
-                if (sv == e.sL) { /* the entry ends in this line: its raw register */                \
-                    const uint32_t reg = finish_lanes<8>(lds, c0, c1, c2, c3);                        \
-                    if (g == 0) {                                                                     \
-                        if (from_start) out[i] = reg;                                                 \
-                        else sa.pfirst[t] = reg;                                                      \
-                    }                                                                                 \
-                    fresh = true;                                                                     \
-                    from_start = true;                                                                \
-                    const bool pin = e.in;                                                            \
-                    const int32_t psL = e.sL;                                                         \
-                    ++i;                                                                              \
-                    /* the next entry's record: from the window loaded four steps ago, or (more */   \
-                    /* than eight entries since) loaded now on a path that waits for itself */        \
-                    const uint32_t k = i - BS;                                                        \
-                    u32x4 rq;                                                                         \
-                    if (k < 8u) {                                                                     \
-                        const int src = lane8 + (int)k;                                                 \
-                        rq.x = (uint32_t)__shfl((int)WS.x, src);                                      \
-                        rq.y = (uint32_t)__shfl((int)WS.y, src);                                      \
-                        rq.z = (uint32_t)__shfl((int)WS.z, src);                                      \
-                        rq.w = (uint32_t)__shfl((int)WS.w, src);                                      \
-                    } else {                                                                          \
-                        rq = ld_rec(i);                                                               \
-                        asm volatile("s_waitcnt vmcnt(0)" : "+v"(rq.x), "+v"(rq.y), "+v"(rq.z), "+v"(rq.w)); \
-                    }                                                                                 \
-                    e = srel(rq, L0, size, mis);                                                      \
-                    r0 = ~rq.w;                                                                       \
-                    const bool sh = pin && e.sF == psL, cont = pin && (sh || e.sF == psL + 1);        \
-                    if (i >= n || !e.in || !cont) live = false; /* a jump: a new tile */              \
-                    else more = sh; /* it starts in this same line */                                 \
-                }                                                                                     \
-            }                                                                                         \
-        }                                                                                             \
-        /* the window first, then the line (a change four steps on waits for neither the line */    \
-        /* just requested nor the ones after it); both refill the registers just used (no copy */    \
-        /* at the loop's back edge). The round's last four steps load the next tile's window. */    \
-        BS = s_ + 4u >= TL ? tf1 + 1u : i + 1u;                                                       \
-        WS = ld_rec((uint64_t)BS + g);                                                                \
-        XS = ld_line(line_of(s_ + 4u));                                                               \
-    }
-
-    for (;;) {  // wave-uniform: a group past the last tile runs empty rounds until its wave is done
-        const bool act = t < ntiles;
-        uint32_t i = tf;
-        SRel e = srel(RA, L0, size, mis);
-        uint32_t r0 = ~RA.w;
-        RA = ld_rec(tf1);
-        bool from_start = k0 == 0u, fresh = true, live = act;
-        uint32_t c0 = 0u, c1 = 0u, c2 = 0u, c3 = 0u;
-        const uint32_t nla = act ? nl : 0u;
-        const uint32_t t2 = t1 + ng;
-        const uint32_t tf2 = sa.tfirst[clampt(t2)], k02 = sa.tk0[clampt(t2)];
-        uint32_t L1 = 0u;
-        uint32_t nl1 = 1u;
-        auto line_of = [&](uint32_t s) -> uint32_t {
-            return s < TL ? L0 + (s < nl ? s : nl - 1u) : L1 + (s - TL < nl1 ? s - TL : nl1 - 1u);
-        };
-        for (uint32_t s0 = 0u; s0 < TL; s0 += 4u) {
-            if (s0 + 4u == TL) {  // the next tile's first lines are loaded from here on
-                L1 = first_line(RA, k01);
-                nl1 = lines_of(t1);
-            }
-            BKD_STREAM_STEP(X0, W0, B0, s0)
-            BKD_STREAM_STEP(X1, W1, B1, s0 + 1u)
-            BKD_STREAM_STEP(X2, W2, B2, s0 + 2u)
-            BKD_STREAM_STEP(X3, W3, B3, s0 + 3u)
-        }
-        if (live && !fresh) {  // the tile ends inside entry i
-            const uint32_t reg = finish_lanes<8>(lds, c0, c1, c2, c3);
-            if (g == 0) {
-                if (from_start) sa.plast[t] = reg;
-                else sa.pfirst[t] = reg;
-            }
-        }
-        t = t1;
-        tf = tf1;
-        k0 = k01;
-        L0 = L1;
-        nl = nl1;
-        t1 = t2;
-        tf1 = tf2;
-        k01 = k02;
-        if (!__any(t < ntiles)) break;
-    }
-#undef BKD_STREAM_STEP
-}
-
 // Chunk kernel of the ragged-batch plan: one chunk per group, grid stride over the descriptor
 // list (sorted by step count, plan_kernels.hpp). Descriptors are read two rounds ahead and each
 // chunk's first loads are issued during the previous chunk (chunk_fold), X/Y register sets
@@ -1623,13 +1336,10 @@ __global__ void __launch_bounds__(kBlock) crc_plan_chunks_kernel(const uint8_t* 
                                                                  const uint32_t* __restrict__ tables,
                                                                  uint32_t* __restrict__ out,
                                                                  uint32_t* __restrict__ partials, OvSrc ov,
-                                                                 PlanRun run, uint32_t* __restrict__ err,
-                                                                 StreamArgs sa, const uint32_t* __restrict__ xinv,
-                                                                 uint32_t poly) {
+                                                                 PlanRun run, uint32_t* __restrict__ err) {
     using Gm = Geo<G>;
     if (!run.plan_entries()) return;  // only short entries
     __shared__ __attribute__((aligned(16))) uint32_t lds[Gm::kLdsWords];
-    if (sa.on() && !run.uniform()) return;  // the stream route: crc_stream_tiles_kernel folds this call
     // near-uniform lengths (PlanRun::uniform): no chunks, every entry whole as in the direct kernel
     ov.all = run.uniform();
     const uint64_t n = ov.all ? 0u : *count;
@@ -1646,27 +1356,6 @@ __global__ void __launch_bounds__(kBlock) crc_plan_chunks_kernel(const uint8_t* 
     const uint64_t nmain = n ? std::min<uint64_t>(n, count[1]) : 0u;
     if (gid < n) plan_chunks_loop<G, PF, NT>(lds, lanereg, g, base, descs, n, nmain, gid, ngroups, out, partials);
     if (nov) groups_loop<G, PF, NT>(lds, lanereg, g, base, ov, nov, gid, ngroups, err);
-}
-
-// The stream route's tile kernel (8-lane groups, persistent grid). Its own launch beside
-// crc_plan_chunks_kernel (each returns at once when plan_scan chose the other route): in one kernel
-// the two loops' registers spilled (128 VGPRs, 36 B of scratch per lane against none apart).
-template <bool NT>
-__global__ void __launch_bounds__(kBlock) crc_stream_tiles_kernel(const uint8_t* __restrict__ base, uint64_t size,
-                                                                  uint64_t n, const uint32_t* __restrict__ tables,
-                                                                  uint32_t* __restrict__ out, PlanRun run, StreamArgs sa,
-                                                                  const uint32_t* __restrict__ xinv, uint32_t poly) {
-    using Gm = Geo<8>;
-    if (!run.plan_entries() || run.uniform() || !sa.on()) return;
-    (void)xinv;
-    (void)poly;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[Gm::kLdsWords];
-    stage_tables<8>(lds, tables);
-    const int lane = threadIdx.x & 63;
-    const uint32_t lanereg = ((uint32_t)(lane & 31) << 2) | (1u << 16);
-    const uint64_t ngroups = (uint64_t)gridDim.x * (kBlock / 8);
-    const uint64_t gid = (uint64_t)blockIdx.x * (kBlock / 8) + (uint64_t)(threadIdx.x / 8);
-    stream_tiles_loop<NT>(lds, lanereg, lane & 7, base, size, sa, n, gid, ngroups, out);
 }
 
 // ---- synthetic input: little-endian splitmix64 stream ----

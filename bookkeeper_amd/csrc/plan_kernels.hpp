@@ -161,112 +161,6 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
     return r;
 }
 
-// ---- stream route: positions (crc_kernels.hpp StreamArgs; model: tests/stream_model.py) ----
-// Entry i maps the stream's end position x (after entries < i) to its own end: x + J' (its new
-// lines), or align(x) + J' when it starts a new tile (a jump). These maps compose in closed form,
-// x -> (f ? align(x + a) : x + a) + b, so positions are an in-order scan (count: per entry block,
-// scan: across blocks, emit: within each block).
-struct SFun {
-    uint32_t f;
-    uint64_t a, b;
-};
-
-__device__ __forceinline__ SFun sf_id() { return SFun{0u, 0u, 0u}; }
-__device__ __forceinline__ uint64_t sf_align(uint64_t x) { return (x + kTileLines - 1u) & ~(uint64_t)(kTileLines - 1u); }
-__device__ __forceinline__ uint64_t sf_apply(const SFun& f, uint64_t x) { return f.f ? sf_align(x + f.a) + f.b : x + f.b; }
-// g first, then h
-__device__ __forceinline__ SFun sf_then(const SFun& g, const SFun& h) {
-    if (!h.f) return SFun{g.f, g.a, g.b + h.b};
-    if (!g.f) return SFun{1u, g.b + h.a, h.b};
-    return SFun{1u, g.a, sf_align(g.b + h.a) + h.b};
-}
-__device__ __forceinline__ SFun sf_shfl_up(const SFun& x, int d) {
-    SFun y;
-    y.f = (uint32_t)__shfl_up((int)x.f, d);
-    y.a = (uint64_t)__shfl_up((unsigned long long)x.a, d);
-    y.b = (uint64_t)__shfl_up((unsigned long long)x.b, d);
-    return y;
-}
-// The element of entry i for the position scan; `sh` / `J1` its shared flag and new lines. (o, l):
-// entry i's offset and length, already loaded (any value when i >= n); the predecessor's come from
-// the neighbouring lane (lane 0 loads them). Called by all threads of the wave.
-__device__ __forceinline__ SFun stream_elem(const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ lengths,
-                                            uint64_t i, uint64_t n, uint64_t size, uint32_t mis, uint64_t o, uint32_t l,
-                                            SEnt& e, bool& sh, bool& jp, uint64_t& J1) {
-    uint64_t po = (uint64_t)__shfl_up((unsigned long long)o, 1);
-    uint32_t pl = (uint32_t)__shfl_up((int)l, 1);
-    if ((threadIdx.x & 63u) == 0u && i > 0u && i - 1u < n) {
-        po = offsets[i - 1u];
-        pl = lengths[i - 1u];
-    }
-    sh = false;
-    jp = false;
-    J1 = 0u;
-    if (i >= n) {
-        e.in = false;
-        return sf_id();
-    }
-    e = stream_ent(o, l, size, mis);
-    if (!e.in) return sf_id();
-    SEnt p;
-    p.in = false;
-    if (i > 0) p = stream_ent(po, pl, size, mis);
-    stream_link(p, e, sh, jp);
-    J1 = (e.Lst - e.F + 1u) - (sh ? 1u : 0u);
-    return SFun{jp ? 1u : 0u, 0u, J1};
-}
-// In-order block scan (1024 threads): this thread's inclusive composition; `total` the block's.
-// A block without a jump (every f = 0, the common case of a packed batch) composes by addition.
-__device__ __forceinline__ SFun block_scan_sf(SFun x, SFun* wt, SFun& total) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (!__syncthreads_or((int)x.f)) {
-        uint64_t v = x.b;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t y = (uint64_t)__shfl_up((unsigned long long)v, d);
-            if (lane >= d) v += y;
-        }
-        if (lane == 63) wt[wave].b = v;
-        __syncthreads();
-        if (threadIdx.x < 64) {  // wave 0 scans the wave totals
-            uint64_t w = lane < kPlanBlock / 64 ? wt[lane].b : 0u, c = w;
-#pragma unroll
-            for (int d = 1; d < kPlanBlock / 64; d <<= 1) {
-                const uint64_t y = (uint64_t)__shfl_up((unsigned long long)c, d);
-                if (lane >= d) c += y;
-            }
-            if (lane < kPlanBlock / 64) wt[lane].a = c - w;  // exclusive prefix of wave `lane`
-            if (lane == kPlanBlock / 64 - 1) wt[kPlanBlock / 64].b = c;
-        }
-        __syncthreads();
-        const SFun r{0u, 0u, wt[wave].a + v};
-        total = SFun{0u, 0u, wt[kPlanBlock / 64].b};
-        __syncthreads();
-        return r;
-    }
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const SFun y = sf_shfl_up(x, d);
-        if (lane >= d) x = sf_then(y, x);
-    }
-    if (lane == 63) wt[wave] = x;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        SFun acc = sf_id();
-        for (int k = 0; k < kPlanBlock / 64; ++k) {
-            const SFun t = wt[k];
-            wt[k] = acc;
-            acc = sf_then(acc, t);
-        }
-        wt[kPlanBlock / 64] = acc;
-    }
-    __syncthreads();
-    const SFun r = sf_then(wt[wave], x);
-    total = wt[kPlanBlock / 64];
-    __syncthreads();
-    return r;
-}
-
 // columns: bins 0 .. nbins-1 (chunk counts by step count; bin JC = full bucket). (Partials need no
 // column of their own: each chunk's partial sits at its own list position.)
 __host__ __device__ __forceinline__ uint32_t plan_ncols(const PlanGeo& pg) { return pg.nbins; }
@@ -278,11 +172,10 @@ __global__ void __launch_bounds__(kPlanBlock) plan_count_kernel(const uint64_t* 
                                                                 const uint32_t* __restrict__ lengths, uint64_t size,
                                                                 uint64_t n, PlanGeo pg, uint32_t* __restrict__ blk,
                                                                 uint32_t* __restrict__ blive, uint32_t nb, PlanRun run,
-                                                                uint32_t* __restrict__ bok, StreamArgs sa) {
+                                                                uint32_t* __restrict__ bok) {
     if (!run.plan_entries()) return;
     __shared__ uint32_t col[kMaxJC + 2];
-    __shared__ uint32_t live, bad, sjumps;
-    __shared__ SFun swt[kPlanBlock / 64 + 1];
+    __shared__ uint32_t live, bad;
     const uint32_t ncols = plan_ncols(pg);
     const uint32_t ref = bok ? lengths[0] : 0u;  // the uniformity ballot's reference length
     for (uint32_t eb = blockIdx.x; eb < nb; eb += gridDim.x) {  // entry blocks of 1024, grid stride
@@ -295,16 +188,12 @@ __global__ void __launch_bounds__(kPlanBlock) plan_count_kernel(const uint64_t* 
     const uint64_t i = (uint64_t)eb * kPlanBlock + threadIdx.x;
     uint32_t full = 0u, mine = 0u;
     bool ok = true;  // length within the band of the reference (PlanRun::in_band)
-    uint64_t oi = 0u;
-    uint32_t li = 0u;
     if (i < n) {
         const uint32_t l = lengths[i];
-        li = l;
         ok = PlanRun::in_band(l, ref);
-        if (!is_small(l, pg)) {  // offsets are read only for the plan's own entries (all of them when
-            mine = 1u;           // the stream route is possible: it has no short class)
-            oi = offsets[i];
-            const EntryPlan p = plan_entry(oi, l, size, pg);
+        if (!is_small(l, pg)) {  // offsets are read only for the plan's own entries
+            mine = 1u;
+            const EntryPlan p = plan_entry(offsets[i], l, size, pg);
             if (p.kind == 0) {
                 if (p.jh != pg.jc) atomicAdd(&col[p.jh], 1u);
                 full = p.full;
@@ -328,23 +217,6 @@ __global__ void __launch_bounds__(kPlanBlock) plan_count_kernel(const uint64_t* 
     if (threadIdx.x == 0) {
         blive[eb] = live;
         if (bok) bok[eb] = bad ^ 1u;
-        sjumps = 0u;
-    }
-    if (sa.sblk) {  // the stream route's position map of this entry block (kernel-uniform)
-        SEnt e;
-        bool sh, jp;
-        uint64_t J1;
-        const SFun el = stream_elem(offsets, lengths, i, n, size, sa.mis, oi, li, e, sh, jp, J1);
-        SFun tot;
-        (void)block_scan_sf(el, swt, tot);  // (its barriers also order sjumps' reset)
-        const uint32_t nj = (uint32_t)__popcll(__ballot(e.in && jp));
-        if ((threadIdx.x & 63) == 0 && nj) atomicAdd(&sjumps, nj);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            sa.sblk[3 * (uint64_t)eb] = tot.a | ((uint64_t)tot.f << 63);
-            sa.sblk[3 * (uint64_t)eb + 1] = tot.b;
-            sa.sblk[3 * (uint64_t)eb + 2] = sjumps;
-        }
     }
     __syncthreads();  // col/live are reset for the next entry block
     }
@@ -360,48 +232,10 @@ __global__ void __launch_bounds__(kPlanBlock) plan_count_kernel(const uint64_t* 
 __global__ void __launch_bounds__(kPlanBlock) plan_scan_kernel(const uint32_t* __restrict__ blk, uint32_t nb,
                                                                uint32_t* __restrict__ blkoff, uint32_t* __restrict__ hdr,
                                                                PlanRun run, uint32_t ncols,
-                                                               const uint32_t* __restrict__ bok, StreamArgs sa) {
+                                                               const uint32_t* __restrict__ bok) {
     if (!run.plan_entries()) return;
     __shared__ uint32_t wsum[kPlanBlock / 64 + 1];
-    __shared__ SFun swt[kPlanBlock / 64 + 1];
-    __shared__ unsigned long long sj;
     const uint32_t c = blockIdx.x;
-    if (sa.sblk && c == ncols + (bok ? 1u : 0u)) {  // the stream route: block positions, then the decision
-        auto fun = [&](uint32_t b) {
-            const uint64_t a = sa.sblk[3 * (uint64_t)b];
-            return SFun{(uint32_t)(a >> 63), a & ~(1ull << 63), sa.sblk[3 * (uint64_t)b + 1]};
-        };
-        const uint32_t per = (nb + kPlanBlock - 1u) / kPlanBlock;
-        const uint32_t b0 = threadIdx.x * per < nb ? threadIdx.x * per : nb;
-        const uint32_t b1 = b0 + per < nb ? b0 + per : nb;
-        SFun acc = sf_id();
-        unsigned long long jumps = 0u;
-        for (uint32_t b = b0; b < b1; ++b) {
-            acc = sf_then(acc, fun(b));
-            jumps += sa.sblk[3 * (uint64_t)b + 2];
-        }
-        if (threadIdx.x == 0) sj = 0u;
-        SFun tot;
-        const SFun inc = block_scan_sf(acc, swt, tot);
-        // runs 0..t composed and applied to position 0 = the end of run t; run t starts where run t-1 ends
-        __shared__ unsigned long long run_end[kPlanBlock];
-        run_end[threadIdx.x] = sf_apply(inc, 0u);
-        atomicAdd(&sj, jumps);
-        __syncthreads();
-        uint64_t pos = threadIdx.x ? run_end[threadIdx.x - 1] : 0u;
-        for (uint32_t b = b0; b < b1; ++b) {
-            sa.sbase[b] = pos;
-            pos = sf_apply(fun(b), pos);
-        }
-        if (threadIdx.x == 0) {
-            const uint64_t end = sf_apply(tot, 0u), tiles = (end + kTileLines - 1u) / kTileLines;
-            sa.shdr[0] = end;
-            sa.shdr[1] = tiles;
-            sa.shdr[2] = sj;
-            *sa.word = (tiles <= sa.cap && sj <= sa.jumps_max) ? sa.epoch : 0u;
-        }
-        return;
-    }
     if (c == ncols) {  // the extra block: PlanRun::uniform for the whole batch
         uint32_t ok = 1u;
         for (uint32_t b = threadIdx.x; b < nb; b += kPlanBlock) ok &= bok[b];
@@ -457,7 +291,7 @@ __global__ void __launch_bounds__(kPlanBlock, BKD_PLAN_OCC) plan_emit_kernel(con
                                                                uint32_t* __restrict__ hdr,
                                                                PlanDesc* __restrict__ descs, uint32_t reps,
                                                                const uint32_t* __restrict__ blive, uint32_t nb,
-                                                               PlanRun run, StreamArgs sa) {
+                                                               PlanRun run) {
     // `reps` virtual blocks per 1024-entry block (few entries, many chunks each: 256 x 16 MiB is one
     // entry block): every replica plans the same entries, replica 0 writes heads, slots and the
     // header, and the replicas split the block's full-chunk descriptors
@@ -469,58 +303,6 @@ __global__ void __launch_bounds__(kPlanBlock, BKD_PLAN_OCC) plan_emit_kernel(con
     __shared__ int64_t st_ae[kPlanBlock], st_s[kPlanBlock];
     __shared__ uint32_t st_m[kPlanBlock], st_flags[kPlanBlock], st_seed[kPlanBlock];
     __shared__ uint32_t s_total;
-    __shared__ SFun swt[kPlanBlock / 64 + 1];
-    if (sa.on()) {
-        // the stream route: each entry's first-line position, its record for the tile kernel, and the
-        // tiles whose first line is one of its new lines (written by the block together, so an entry
-        // of thousands of tiles costs no serial loop); replicas split those writes by position
-        for (uint32_t vb = blockIdx.x; vb < nb * reps; vb += gridDim.x) {
-            const uint32_t eb = vb / reps, rep = vb - eb * reps;
-            const uint64_t i = (uint64_t)eb * kPlanBlock + threadIdx.x;
-            SEnt e;
-            bool sh, jp;
-            uint64_t J1;
-            const uint64_t o = i < n ? offsets[i] : 0u;
-            const uint32_t l = i < n ? lengths[i] : 0u;
-            const SFun el = stream_elem(offsets, lengths, i, n, size, sa.mis, o, l, e, sh, jp, J1);
-            SFun tot;
-            const SFun inc = block_scan_sf(el, swt, tot);
-            const uint64_t V = sf_apply(inc, sa.sbase[eb]) - J1;  // its first new line
-            const uint64_t P0 = V - (sh ? 1u : 0u);                 // its first line
-            if (rep == 0u && i < n) {
-                sa.spos[i] = e.in ? P0 : (1ull << 63);
-                sa.srec[i] = u32x4{(uint32_t)o, (uint32_t)(o >> 32), l, seeds ? seeds[i] : seed_all};
-            }
-            uint32_t cnt = 0u;
-            uint64_t tf0 = 0u;
-            if (e.in && J1) {
-                tf0 = (V + kTileLines - 1u) / kTileLines;
-                const uint64_t tl = (V + J1 - 1u) / kTileLines;
-                cnt = tl >= tf0 ? (uint32_t)(tl - tf0 + 1u) : 0u;
-            }
-            uint32_t tb;
-            const uint32_t ex = block_excl_scan(cnt, wsum, tb);
-            exf[threadIdx.x] = ex;
-            if (threadIdx.x == 0) exf[kPlanBlock] = tb;
-            st_ae[threadIdx.x] = (int64_t)tf0;
-            st_s[threadIdx.x] = (int64_t)P0;
-            __syncthreads();
-            const uint32_t k0 = (uint32_t)((uint64_t)tb * rep / reps), k1 = (uint32_t)((uint64_t)tb * (rep + 1u) / reps);
-            for (uint32_t k = k0 + threadIdx.x; k < k1; k += kPlanBlock) {
-                uint32_t lo = 0u, hi = kPlanBlock;  // owner: the last thread t with exf[t] <= k
-                while (hi - lo > 1u) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (exf[mid] <= k) lo = mid;
-                    else hi = mid;
-                }
-                const uint64_t tt = (uint64_t)st_ae[lo] + (k - exf[lo]);
-                sa.tfirst[tt] = (uint32_t)((uint64_t)eb * kPlanBlock + lo);
-                sa.tk0[tt] = (uint32_t)(tt * kTileLines - (uint64_t)st_s[lo]);
-            }
-            __syncthreads();  // the stashes are rewritten by the next virtual block
-        }
-        return;
-    }
     const uint32_t ncols = plan_ncols(pg);
     for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) bin0[k] = hdr[kHdrBase + k];
     __syncthreads();
@@ -641,6 +423,28 @@ struct PlanDirectSrc {
     }
 };
 
+// a * b mod P, bitwise (no tables): 32 shift/xor steps, for the few products per entry that have
+// no operator table (x^(-8*pad), powers of X).
+__device__ __forceinline__ uint32_t gf_mul_bits(uint32_t a, uint32_t b, uint32_t poly) {
+    uint32_t prod = 0u, cur = b;
+#pragma unroll
+    for (int k = 31; k >= 0; --k) {
+        prod ^= ((a >> k) & 1u) ? cur : 0u;
+        cur = (cur >> 1) ^ ((cur & 1u) ? poly : 0u);
+    }
+    return prod;
+}
+
+__device__ __forceinline__ uint32_t gf_pow_bits(uint32_t x, uint32_t e, uint32_t poly) {
+    uint32_t r = 0x80000000u;  // x^0
+    while (e) {
+        if (e & 1u) r = gf_mul_bits(r, x, poly);
+        x = gf_mul_bits(x, x, poly);
+        e >>= 1;
+    }
+    return r;
+}
+
 // Horner over the partial registers of each chunked entry, then x^(-8*pad); serial fold of
 // entries the plan did not chunk. Entries with more than kCombineSerial chunks are combined by a
 // wave (up to kCombineWave chunks) or by the whole block (e.g. one 64 MiB entry = 16 Ki chunks)
@@ -729,7 +533,7 @@ __global__ void __launch_bounds__(1024, BKD_PLAN_OCC) plan_combine_kernel(
     const uint32_t* __restrict__ btab, const uint32_t* __restrict__ xinv, uint32_t poly,
     const uint32_t* __restrict__ pslot, const uint32_t* __restrict__ hslot, const uint32_t* __restrict__ partials,
     uint32_t* __restrict__ out, uint32_t* __restrict__ err, uint32_t reps, const uint32_t* __restrict__ blive,
-    uint32_t nblk, PlanRun run, StreamArgs sa, const uint32_t* __restrict__ xline) {
+    uint32_t nblk, PlanRun run) {
     // `reps` virtual blocks per 1024-entry block (as plan_emit_kernel): each replica lists the
     // block's entries of > kCombineSerial chunks and combines its share of them; replica 0 does the
     // rest (invalid and serial entries are idempotent writes, cheap, and left to every replica).
@@ -744,118 +548,6 @@ __global__ void __launch_bounds__(1024, BKD_PLAN_OCC) plan_combine_kernel(
     for (int k = threadIdx.x; k < 1024; k += blockDim.x) X[k] = xtab[k];
     build_slice16(T, btab);
     const uint32_t nvb = nblk * reps;
-    if (sa.on()) {
-        // the stream route (xtab = x^(8 * 4096), one tile): an entry whose lines span tiles t0 < t1
-        // is plast[t0], pfirst[t0 + 1 .. t1 - 1] (whole tiles) joined by Horner with X, then
-        // * x^(1024 L) ^ pfirst[t1] (its last L lines), then * x^(-8 pad). Entries outside the
-        // stream (empty, a padded message under 4 bytes, out of range) are done here one thread each;
-        // an entry inside one tile has its raw register in out[i] (pad product and inversion here).
-        auto piece = [&](uint64_t t0, uint64_t t1, uint32_t m, uint32_t c) -> uint32_t {  // weight X^c
-            return c + 1u == m ? sa.plast[t0] : sa.pfirst[t1 - 1u - c];
-        };
-        for (uint32_t vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
-            const uint32_t eb = vb / reps, rep = vb - eb * reps;
-            if (threadIdx.x == 0) nbig = 0u;
-            __syncthreads();
-            const uint64_t i = (uint64_t)eb * blockDim.x + threadIdx.x;
-            uint32_t is_big = 0u;
-            if (i < n) {
-                const uint64_t pos = sa.spos[i];
-                const uint64_t o = offsets[i];
-                const uint32_t l = lengths[i];
-                if (pos >> 63) {
-                    if (rep == 0u) {
-                        if (!entry_valid(o, l, size)) {
-                            out[i] = 0u;
-                            if (err) atomicOr(err, 1u);
-                        } else {
-                            const uint32_t reg = ~(seeds ? seeds[i] : seed_all);
-                            out[i] = l ? ~serial_crc(base, o, l, reg, T) : ~reg;
-                        }
-                    }
-                } else {
-                    const SEnt e = stream_ent(o, l, size, sa.mis);
-                    const uint64_t P1 = pos + (e.Lst - e.F), t0 = pos / kTileLines, t1 = P1 / kTileLines;
-                    const uint64_t m = t1 - t0;  // pieces before the last
-                    if (m > kCombineSerial) {
-                        is_big = 1u;
-                        if (reps == 1u) big[atomicAdd(&nbig, 1u)] = (uint32_t)threadIdx.x;
-                    } else if (m == 0u) {  // inside one tile: the tile kernel left its raw register
-                        if (rep == 0u) {
-                            const uint32_t reg = out[i];
-                            out[i] = ~(e.pad ? gf_mul_bits(xinv[e.pad], reg, poly) : reg);
-                        }
-                    } else if (rep == 0u) {
-                        uint32_t reg = piece(t0, t1, (uint32_t)m, (uint32_t)m - 1u);
-                        for (int c0 = (int)m - 2; c0 >= 0; c0 -= 8) {
-                            uint32_t pv[8];
-#pragma unroll
-                            for (int k = 0; k < 8; ++k) pv[k] = c0 - k >= 0 ? piece(t0, t1, (uint32_t)m, (uint32_t)(c0 - k)) : 0u;
-#pragma unroll
-                            for (int k = 0; k < 8; ++k)
-                                if (c0 - k >= 0) reg = mul_x(X, reg) ^ pv[k];
-                        }
-                        reg = gf_mul_bits(xline[P1 - t1 * kTileLines + 1u], reg, poly) ^ sa.pfirst[t1];
-                        if (e.pad) reg = gf_mul_bits(xinv[e.pad], reg, poly);
-                        out[i] = ~reg;
-                    }
-                }
-            }
-            uint32_t nb;
-            if (reps > 1u) {
-                const uint32_t bpos = block_excl_scan(is_big, wsum, nb);
-                if (is_big) big[bpos] = (uint32_t)threadIdx.x;
-                __syncthreads();
-            } else {
-                __syncthreads();
-                nb = nbig;
-            }
-            // entries of more than kCombineSerial tiles: a wave each up to kCombineWave, else the block
-            const uint32_t lane = threadIdx.x & 63u, nwaves = blockDim.x >> 6;
-            for (uint32_t k = rep * nwaves + (threadIdx.x >> 6); k < nb; k += reps * nwaves) {
-                const uint64_t ie = (uint64_t)eb * blockDim.x + big[k];
-                const SEnt e = stream_ent(offsets[ie], lengths[ie], size, sa.mis);
-                const uint64_t pos = sa.spos[ie], P1 = pos + (e.Lst - e.F), t0 = pos / kTileLines, t1 = P1 / kTileLines;
-                const uint32_t m = (uint32_t)(t1 - t0);
-                if (m > kCombineWave) continue;  // wave-uniform
-                const uint32_t per = (m + 63u) >> 6, lo = lane * per, hi = lo + per < m ? lo + per : m;
-                uint32_t r = 0u;
-                for (int c = (int)hi - 1; c >= (int)lo; --c) r = mul_x(X, r) ^ piece(t0, t1, m, (uint32_t)c);
-                if (lo < hi && lo) r = gf_mul_bits(gf_pow_bits(xval, lo, poly), r, poly);
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) r ^= (uint32_t)__shfl_xor((int)r, d);
-                if (lane == 0u) {
-                    r = gf_mul_bits(xline[P1 - t1 * kTileLines + 1u], r, poly) ^ sa.pfirst[t1];
-                    out[ie] = ~(e.pad ? gf_mul_bits(xinv[e.pad], r, poly) : r);
-                }
-            }
-            for (uint32_t k = rep; k < nb; k += reps) {
-                const uint64_t ie = (uint64_t)eb * blockDim.x + big[k];
-                const SEnt e = stream_ent(offsets[ie], lengths[ie], size, sa.mis);
-                const uint64_t pos = sa.spos[ie], P1 = pos + (e.Lst - e.F), t0 = pos / kTileLines, t1 = P1 / kTileLines;
-                const uint32_t m = (uint32_t)(t1 - t0);
-                if (m <= kCombineWave) continue;  // block-uniform
-                const uint32_t per = (m + blockDim.x - 1u) / blockDim.x, lo = threadIdx.x * per,
-                               hi = lo + per < m ? lo + per : m;
-                uint32_t r = 0u;
-                for (int c = (int)hi - 1; c >= (int)lo; --c) r = mul_x(X, r) ^ piece(t0, t1, m, (uint32_t)c);
-                if (lo < hi && lo) r = gf_mul_bits(gf_pow_bits(xval, lo, poly), r, poly);
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) r ^= (uint32_t)__shfl_xor((int)r, d);
-                if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = r;
-                __syncthreads();
-                if (threadIdx.x == 0) {
-                    uint32_t reg = 0u;
-                    for (uint32_t w = 0; w < blockDim.x / 64; ++w) reg ^= red[w];
-                    reg = gf_mul_bits(xline[P1 - t1 * kTileLines + 1u], reg, poly) ^ sa.pfirst[t1];
-                    out[ie] = ~(e.pad ? gf_mul_bits(xinv[e.pad], reg, poly) : reg);
-                }
-                __syncthreads();
-            }
-            __syncthreads();  // big[] and nbig are rebuilt by the next virtual block
-        }
-        return;
-    }
     for (uint32_t vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
     const uint32_t eb = vb / reps, rep = vb - eb * reps;
     if (blive[eb] == 0u) continue;  // only short entries: the short-entry launch wrote them

@@ -1,0 +1,559 @@
+// The stream route for ragged indexed batches (DESIGN.md §3 "Stream route"; CPU model of the same
+// decomposition, step by step: tests/stream_model.py RangeModel, checked against the oracle on
+// packed, gappy, unsorted and overlapping indexes).
+//
+// The entries' 128-byte device lines are laid end to end in index order: entry i takes the next J'
+// positions of the stream, J' = its lines minus one when its first line is the previous entry's
+// last (that line is folded once, into both). Positions are a plain prefix sum of J'. Group r of the
+// tile kernel folds the positions [r TL, (r + 1) TL), TL = ceil(end / groups): each line is loaded
+// once and folded into every entry it holds, the bytes outside an entry zeroed in the very register
+// that is folded. An entry inside one range gets its raw register there; the pieces of a longer
+// entry (one raw register per range) are joined by stream_combine_kernel with x^(1024 TL) per range
+// and x^(1024 L) for its last L lines, then x^(-8 pad).
+//
+// Three launches, no host sync: plan_stream_kernel (positions: per-block sums and a decoupled
+// look-back across blocks, then each entry's position and record) -> crc_stream_ranges_kernel ->
+// stream_combine_kernel. Chunked-plan equivalent: crc32c_sse42.cpp:92-134 cuts one buffer into
+// chunks folded in parallel and merged by shift tables; here a batch's entries are cut into equal
+// ranges of lines across the whole chip and merged the same way.
+#pragma once
+#include "plan_kernels.hpp"
+
+namespace bkd {
+
+#ifndef BKD_STREAM
+#define BKD_STREAM 1  // 0: ragged batches keep the chunked plan (A/B builds)
+#endif
+constexpr uint64_t kStreamMaxTL = 1ull << 22;  // lines per range (above: every entry whole, one per group)
+
+struct StreamArgs {
+    uint64_t* sdesc;   // [nb] look-back words of the entry blocks: epoch | status | value
+    uint64_t* shdr;    // [0] the stream's end (positions)
+    uint64_t* spos;    // [n] V (first new line's position) | shared << 62 | outside the stream << 63
+    u32x4* srec;       // [n] {offset lo, offset hi, length, seed}
+    uint32_t* pfirst;  // [ngroups] raw register of a range's first piece (its entry began before it)
+    uint32_t* plast;   // [ngroups] raw register of a range's last piece (its entry goes on after it)
+    uint32_t* ticket;  // entry-block ticket of plan_stream_kernel (0 between calls)
+    uint32_t ngroups;  // ranges = 8-lane groups of the tile kernel
+    uint32_t mis;      // device address of base modulo 128
+    uint32_t epoch;    // the call's epoch (look-back words of earlier calls never match)
+    uint64_t maxtl;    // lines per range above which every entry is taken whole (kStreamMaxTL; tests lower it)
+};
+
+__host__ __device__ __forceinline__ uint64_t stream_range_len(uint64_t end, uint64_t ngroups) {
+    uint64_t tl = (end + ngroups - 1u) / ngroups;
+    if (tl == 0u) tl = 1u;
+    return (tl + 3u) & ~3ull;  // a multiple of the tile loop's four line sets
+}
+
+// Stream geometry of one entry (stream_model.Geo).
+struct SEnt {
+    uint64_t F, Lst;  // first and last device line
+    uint32_t d, pad;  // bytes of its first line before the entry; bytes of its last line after it
+    bool in;          // in the stream: valid, non-empty, padded message of >= 4 bytes (the seed image)
+};
+
+__device__ __forceinline__ SEnt stream_ent(uint64_t o, uint32_t l, uint64_t size, uint32_t mis) {
+    SEnt e;
+    const uint64_t as = (uint64_t)mis + o, ae = as + l;
+    e.F = as >> 7;
+    e.Lst = l ? (ae - 1u) >> 7 : e.F;
+    e.d = (uint32_t)(as & 127u);
+    e.pad = (128u - (uint32_t)(ae & 127u)) & 127u;
+    e.in = !(o > size || (uint64_t)l > size - o) && l != 0u && l + e.pad >= 4u;
+    return e;
+}
+
+// ---- positions: plan_stream_kernel ----
+// look-back word: epoch (20 bits) | status (2: 1 = block aggregate, 2 = inclusive prefix) | value (42)
+__device__ __forceinline__ uint64_t sd_pack(uint32_t epoch, uint32_t st, uint64_t v) {
+    return ((uint64_t)(epoch & 0xFFFFFu) << 44) | ((uint64_t)st << 42) | (v & ((1ull << 42) - 1u));
+}
+
+// One 1024-thread block per entry block, taken by ticket in the order the blocks start (so a block
+// waiting on its predecessors waits only for blocks already running). Per entry: in the stream?, shared with the
+// previous entry?, J'; a block scan; the block's aggregate published at once, then a look-back by
+// wave 0 over the preceding blocks' words (64 at a time: aggregates summed until an inclusive prefix)
+// and the block's own prefix published. The look-back words are device-scope atomics: the value
+// travels in the word that carries its status, so no fence or cache write-back is needed on this
+// multi-XCD part. Then each entry's position and record; the last block writes the end.
+__global__ void __launch_bounds__(kPlanBlock) plan_stream_kernel(const uint64_t* __restrict__ offsets,
+                                                                 const uint32_t* __restrict__ lengths,
+                                                                 const uint32_t* __restrict__ seeds, uint32_t seed_all,
+                                                                 uint64_t size, uint64_t n, uint32_t nb, StreamArgs sa) {
+    __shared__ uint64_t wtot[kPlanBlock / 64];
+    __shared__ uint64_t s_prefix;
+    __shared__ uint32_t s_eb;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t ep = sa.epoch & 0xFFFFFu;
+    if (threadIdx.x == 0) s_eb = atomicAdd(sa.ticket, 1u);  // (stream_combine_kernel resets it)
+    __syncthreads();
+    {
+        const uint32_t eb = s_eb;
+        const uint64_t i = (uint64_t)eb * kPlanBlock + threadIdx.x;
+        const uint64_t o = i < n ? offsets[i] : 0u;
+        const uint32_t l = i < n ? lengths[i] : 0u;
+        uint64_t po = (uint64_t)__shfl_up((unsigned long long)o, 1);
+        uint32_t pl = (uint32_t)__shfl_up((int)l, 1);
+        if (lane == 0 && i > 0u && i - 1u < n) {
+            po = offsets[i - 1u];
+            pl = lengths[i - 1u];
+        }
+        SEnt e = stream_ent(o, l, size, sa.mis);
+        if (i >= n) e.in = false;
+        bool sh = false;
+        if (e.in && i > 0u) {
+            const SEnt p = stream_ent(po, pl, size, sa.mis);
+            sh = p.in && e.F == p.Lst;
+        }
+        const uint64_t jn = e.in ? e.Lst - e.F + 1u - (sh ? 1u : 0u) : 0u;
+        // block inclusive scan of jn
+        uint64_t v = jn;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t y = (uint64_t)__shfl_up((unsigned long long)v, d);
+            if (lane >= d) v += y;
+        }
+        if (lane == 63) wtot[wave] = v;
+        __syncthreads();
+        uint64_t wpre = 0u, agg = 0u;
+        for (int k = 0; k < kPlanBlock / 64; ++k) {
+            const uint64_t t = wtot[k];
+            wpre += k < wave ? t : 0u;
+            agg += t;
+        }
+        if (wave == 0) {  // publish the aggregate, look back, publish the prefix
+            if (lane == 0)
+                __hip_atomic_store(&sa.sdesc[eb], sd_pack(ep, eb ? 1u : 2u, agg), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            uint64_t prefix = 0u;
+            int64_t top = (int64_t)eb - 1;  // the look-back window ends at block `top`
+            while (top >= 0) {
+                const int64_t p = top - lane;
+                uint64_t w = 0u;
+                bool ready = true;
+                if (p >= 0) {
+                    w = __hip_atomic_load(&sa.sdesc[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ready = (uint32_t)(w >> 44) == ep && ((w >> 42) & 3u) != 0u;
+                }
+                // the nearest inclusive prefix in the window (lanes in order of distance)
+                const uint64_t pmask = __ballot(p >= 0 && ready && ((w >> 42) & 3u) == 2u);
+                const int stop = pmask ? __builtin_ctzll(pmask) : 64;
+                // every word up to it must be there; otherwise wait and read the window again
+                const uint64_t rmask = __ballot(ready);
+                const uint64_t need = stop >= 63 ? ~0ull : ((2ull << stop) - 1u);
+                if ((rmask & need) != need) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                uint64_t part = (p >= 0 && lane <= stop) ? (w & ((1ull << 42) - 1u)) : 0u;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) part += (uint64_t)__shfl_xor((unsigned long long)part, d);
+                prefix += part;
+                if (stop < 64) break;
+                top -= 64;
+            }
+            if (lane == 0) {
+                if (eb)
+                    __hip_atomic_store(&sa.sdesc[eb], sd_pack(ep, 2u, prefix + agg), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                s_prefix = prefix;
+                if (eb == nb - 1u) sa.shdr[0] = prefix + agg;
+            }
+        }
+        __syncthreads();
+        if (i < n) {
+            const uint64_t V = s_prefix + wpre + v - jn;
+            sa.spos[i] = V | ((uint64_t)sh << 62) | ((uint64_t)!e.in << 63);
+            sa.srec[i] = u32x4{(uint32_t)o, (uint32_t)(o >> 32), l, seeds ? seeds[i] : seed_all};
+        }
+    }
+}
+
+// ---- the tile kernel ----
+// Keeps bytes [a, b) of a 16-byte block (block coordinates, any range), zeroes the rest.
+__device__ __forceinline__ u32x4 keep_range(u32x4 w, int32_t a, int32_t b) {
+    auto m = [](uint32_t x, int32_t lo, int32_t hi) -> uint32_t {  // (selects, no branches)
+        const int32_t a = lo < 0 ? 0 : lo, b = hi > 4 ? 4 : hi, wd = b - a;
+        const uint32_t msk = (0xFFFFFFFFu >> ((uint32_t)(32 - 8 * wd) & 31u)) << ((uint32_t)(8 * a) & 31u);
+        return wd > 0 ? x & msk : 0u;
+    };
+    w.x = m(w.x, a, b);
+    w.y = m(w.y, a - 4, b - 4);
+    w.z = m(w.z, a - 8, b - 8);
+    w.w = m(w.w, a - 12, b - 12);
+    return w;
+}
+
+// An entry's record decoded for the fold, relative to its range: byte 0 = the first byte of the
+// range's first position; its first line at position pF (may be negative: it began in an earlier
+// range). Bytes clamped to +-2^30 and positions to +-2^29 (an entry that far away never meets them).
+struct SRel {
+    int32_t a, e;    // first byte and end
+    int32_t sF, sL;  // positions of its first and last line
+    uint32_t d;      // bytes of its first line before it
+    uint32_t lst;    // device line of its last line
+    uint32_t F;      // device line of its first line
+    bool in;         // in the stream
+};
+
+__device__ __forceinline__ SRel srel(const u32x4& r, int64_t pF, uint64_t size, uint32_t mis) {
+    const uint64_t o = (uint64_t)r.x | ((uint64_t)r.y << 32);
+    const uint32_t l = r.z;
+    const uint64_t as = (uint64_t)mis + o;
+    const uint64_t F = as >> 7, Lst = l ? (as + l - 1u) >> 7 : F;
+    SRel q;
+    q.d = (uint32_t)(as & 127u);
+    const int64_t A = pF * 128 + (int64_t)q.d, E = A + (int64_t)l, PL = pF + (int64_t)(Lst - F);
+    auto cl = [](int64_t v, int64_t m) -> int32_t { return (int32_t)(v < -m ? -m : (v > m ? m : v)); };
+    q.a = cl(A, 1 << 30);
+    q.e = cl(E, 1 << 30);
+    q.sF = cl(pF, 1 << 29);
+    q.sL = cl(PL, 1 << 29);
+    q.F = (uint32_t)F;
+    q.lst = (uint32_t)Lst;
+    const uint32_t pad = (128u - (uint32_t)((as + l) & 127u)) & 127u;
+    q.in = !(o > size || (uint64_t)l > size - o) && l != 0u && l + pad >= 4u;
+    return q;
+}
+
+// Device lines of a record: first, last, in the stream.
+struct SLines {
+    uint32_t F, Lst;
+    bool in;
+};
+__device__ __forceinline__ SLines slines(const u32x4& r, uint64_t size, uint32_t mis) {
+    const uint64_t o = (uint64_t)r.x | ((uint64_t)r.y << 32);
+    const uint32_t l = r.z;
+    const uint64_t as = (uint64_t)mis + o;
+    SLines q;
+    q.F = (uint32_t)(as >> 7);
+    q.Lst = l ? (uint32_t)((as + l - 1u) >> 7) : q.F;
+    const uint32_t pad = (128u - (uint32_t)((as + l) & 127u)) & 127u;
+    q.in = !(o > size || (uint64_t)l > size - o) && l != 0u && l + pad >= 4u;
+    return q;
+}
+
+// One range per 8-lane group. Four register sets hold the lines of the next four positions, loaded
+// by a cursor that walks the entries' records four positions ahead of the fold (the device line of
+// a position is its entry's first new line plus the steps since). Beside every line the group loads
+// a window of the eight records after the cursor's entry, one per lane (`W`, base index `B`), used
+// four steps later by the cursor and by the fold (an entry change takes its record with a group
+// shuffle). Only when more than eight entries begin within four positions (entries of under half a
+// line) is a record loaded on the spot, on a path that waits for itself. Every load of the common
+// path is unconditional and at a fixed point of the step, so the compiler's memory waits stay
+// counted (no drain of the lines in flight); the loop body is the four steps of one line set.
+template <bool NT>
+__device__ __forceinline__ void stream_ranges_loop(const uint32_t* lds, uint32_t lanereg, int g,
+                                                   const uint8_t* __restrict__ base, uint64_t size,
+                                                   const StreamArgs& sa, uint64_t n, uint64_t r, uint64_t TL,
+                                                   uint64_t end, uint32_t* __restrict__ out) {
+    const uint8_t* lb = base - sa.mis;  // device line 0 (the line holding base)
+    const uint32_t lmax = (uint32_t)(((uint64_t)sa.mis + size - 1u) >> 7);
+    const uint32_t mis = sa.mis;
+    const int lane8 = (int)(threadIdx.x & 56u);  // the group's first lane in its wave
+    const uint32_t n32 = (uint32_t)n;
+    auto ld_line = [&](uint32_t L) { return ld16<NT>(lb + ((uint64_t)(L < lmax ? L : lmax) << 7) + 16 * g); };
+    auto ld_rec = [&](uint32_t i) { return sa.srec[i < n32 ? i : n32 - 1u]; };
+    auto vpos = [&](uint64_t j) { return sa.spos[j] & ((1ull << 62) - 1u); };
+
+    const uint64_t R0 = r * TL;
+    const bool act = R0 < end;
+    const uint32_t nla = act ? (uint32_t)(end - R0 < TL ? end - R0 : TL) : 0u;
+    // the range's first entry: the last j with V_j <= R0 (V is non-decreasing), 8-ary by the group
+    uint64_t lo = 0u, hi = act ? n : 1u;
+    while (__any(hi - lo > 1u)) {
+        const uint64_t span = hi - lo, step = span > 1u ? (span + 7u) / 8u : 1u;
+        const uint64_t probe = lo + (uint64_t)(g + 1) * step;
+        const bool le = span > 1u && probe < hi && vpos(probe) <= R0;
+        const uint32_t bits = (uint32_t)(__ballot(le) >> lane8) & 0xFFu;
+        const uint32_t c = (uint32_t)__popc(bits);
+        if (span > 1u) {
+            const uint64_t nhi = lo + (uint64_t)(c + 1u) * step;
+            lo += (uint64_t)c * step;
+            hi = nhi < hi ? nhi : hi;
+        }
+    }
+    const uint32_t j0 = (uint32_t)lo;
+    const uint64_t sp0 = sa.spos[j0];
+    const u32x4 rec0 = ld_rec(j0);
+    const int64_t P0 = (int64_t)(sp0 & ((1ull << 62) - 1u)) - (int64_t)((sp0 >> 62) & 1u);  // its first line
+    // fold state
+    uint32_t i = j0;
+    SRel e = srel(rec0, P0 - (int64_t)R0, size, mis);
+    uint32_t r0 = ~rec0.w;
+    bool from_start = P0 >= (int64_t)R0, fresh = true, live = act, pin = true;
+    uint32_t c0 = 0u, c1 = 0u, c2 = 0u, c3 = 0u;
+    // cursor: entry cj, device line cL of its position, crem new lines of cj after it, cpin: the
+    // index before the next one looked at is in the stream
+    uint32_t cj = j0, cL = e.F + (uint32_t)((int64_t)R0 - P0), crem = e.lst - cL;
+    bool cpin = true;
+    // the cursor's next position (records from window (WS, BS), or loaded on the spot)
+    auto advance = [&](const u32x4& WS, uint32_t BS) {
+        if (crem > 0u) {
+            ++cL;
+            --crem;
+            return;
+        }
+        for (;;) {  // group-uniform
+            const uint32_t j = cj + 1u;
+            if (j >= n32) {  // past the last entry: a clamped line, never folded
+                cj = n32;
+                break;
+            }
+            const uint32_t k = j - BS;
+            u32x4 rq;
+            if (k < 8u) {
+                const int src = lane8 + (int)k;
+                rq.x = (uint32_t)__shfl((int)WS.x, src);
+                rq.y = (uint32_t)__shfl((int)WS.y, src);
+                rq.z = (uint32_t)__shfl((int)WS.z, src);
+                rq.w = (uint32_t)__shfl((int)WS.w, src);
+            } else {
+                rq = ld_rec(j);
+                asm volatile("s_waitcnt vmcnt(0)" : "+v"(rq.x), "+v"(rq.y), "+v"(rq.z), "+v"(rq.w));
+            }
+            cj = j;
+            const SLines q = slines(rq, size, mis);
+            if (!q.in) {
+                cpin = false;
+                continue;
+            }
+            const bool sh = cpin && q.F == cL;
+            cpin = true;
+            if (sh && q.Lst == q.F) continue;  // inside the current line: no position of its own
+            cL = q.F + (sh ? 1u : 0u);
+            crem = q.Lst - cL;
+            break;
+        }
+    };
+    // prologue: the range's first four positions (records loaded on the spot: a window based past
+    // the end forces it)
+    const u32x4 none{0u, 0u, 0u, 0u};
+    u32x4 X0 = ld_line(cL), W0 = ld_rec(cj + 1u + (uint32_t)g);
+    uint32_t B0 = cj + 1u;
+    advance(none, 0xFFFFFFF0u);
+    u32x4 X1 = ld_line(cL), W1 = ld_rec(cj + 1u + (uint32_t)g);
+    uint32_t B1 = cj + 1u;
+    advance(none, 0xFFFFFFF0u);
+    u32x4 X2 = ld_line(cL), W2 = ld_rec(cj + 1u + (uint32_t)g);
+    uint32_t B2 = cj + 1u;
+    advance(none, 0xFFFFFFF0u);
+    u32x4 X3 = ld_line(cL), W3 = ld_rec(cj + 1u + (uint32_t)g);
+    uint32_t B3 = cj + 1u;
+
+#define BKD_STREAM_STEP(XS, WS, BS, S)                                                                \
+    {                                                                                                 \
+        const uint32_t s_ = (S);                                                                      \
+        const u32x4 w = XS;                                                                           \
+        bool more = live && s_ < nla;                                                                 \
+        while (__any(more)) {                                                                         \
+            if (more) {                                                                               \
+                const int32_t sv = (int32_t)s_;                                                       \
+                const int32_t lbase = 128 * sv + 16 * g;                                              \
+                u32x4 wm = w;                                                                         \
+                if (sv == e.sF || sv == e.sL) wm = keep_range(w, e.a - lbase, e.e - lbase);           \
+                if (sv == e.sF) {                                                                     \
+                    const int64_t dd = (int64_t)e.d - 16 * g;                                         \
+                    wm.x ^= place_seed(r0, dd);                                                       \
+                    wm.y ^= place_seed(r0, dd - 4);                                                   \
+                    wm.z ^= place_seed(r0, dd - 8);                                                   \
+                    wm.w ^= place_seed(r0, dd - 12);                                                  \
+                }                                                                                     \
+                if (sv == e.sF + 1 && e.d > 124u && g == 0) wm.x ^= place_seed(r0, (int64_t)e.d - 128); \
+                const uint32_t m0 = mul_main_add(lds, c0, lanereg, wm.x);                             \
+                const uint32_t m1 = mul_main_add(lds, c1, lanereg, wm.y);                             \
+                const uint32_t m2 = mul_main_add(lds, c2, lanereg, wm.z);                             \
+                const uint32_t m3 = mul_main_add(lds, c3, lanereg, wm.w);                             \
+                c0 = fresh ? wm.x : m0;                                                               \
+                c1 = fresh ? wm.y : m1;                                                               \
+                c2 = fresh ? wm.z : m2;                                                               \
+                c3 = fresh ? wm.w : m3;                                                               \
+                fresh = false;                                                                        \
+                more = false;                                                                         \
+                if (sv == e.sL) { /* the entry ends in this line: its raw register */                \
+                    const uint32_t reg = finish_lanes<8>(lds, c0, c1, c2, c3);                        \
+                    if (g == 0) {                                                                     \
+                        if (from_start) out[i] = reg;                                                 \
+                        else sa.pfirst[r] = reg;                                                      \
+                    }                                                                                 \
+                    fresh = true;                                                                     \
+                    from_start = true;                                                                \
+                    const uint32_t plst = e.lst;                                                      \
+                    for (;;) { /* the next entry of the stream (group-uniform) */                    \
+                        ++i;                                                                          \
+                        if (i >= n32) {                                                               \
+                            live = false;                                                             \
+                            break;                                                                    \
+                        }                                                                             \
+                        const uint32_t k = i - BS;                                                    \
+                        u32x4 rq;                                                                     \
+                        if (k < 8u) {                                                                 \
+                            const int src = lane8 + (int)k;                                           \
+                            rq.x = (uint32_t)__shfl((int)WS.x, src);                                  \
+                            rq.y = (uint32_t)__shfl((int)WS.y, src);                                  \
+                            rq.z = (uint32_t)__shfl((int)WS.z, src);                                  \
+                            rq.w = (uint32_t)__shfl((int)WS.w, src);                                  \
+                        } else {                                                                      \
+                            rq = ld_rec(i);                                                           \
+                            asm volatile("s_waitcnt vmcnt(0)" : "+v"(rq.x), "+v"(rq.y), "+v"(rq.z), "+v"(rq.w)); \
+                        }                                                                             \
+                        const SLines q = slines(rq, size, mis);                                       \
+                        if (!q.in) {                                                                  \
+                            pin = false;                                                              \
+                            continue;                                                                 \
+                        }                                                                             \
+                        const bool sh = pin && q.F == plst;                                           \
+                        pin = true;                                                                   \
+                        e = srel(rq, (int64_t)sv + (sh ? 0 : 1), size, mis);                          \
+                        r0 = ~rq.w;                                                                   \
+                        more = sh; /* it starts in this same line */                                  \
+                        break;                                                                        \
+                    }                                                                                 \
+                }                                                                                     \
+            }                                                                                         \
+        }                                                                                             \
+        /* the cursor moves to position s + 4 with this slot's window; then the slot is refilled: */ \
+        /* the window first, then the line (neither is waited for before its own use) */             \
+        advance(WS, BS);                                                                              \
+        BS = cj + 1u;                                                                                 \
+        WS = ld_rec(BS + (uint32_t)g);                                                                \
+        XS = ld_line(cL);                                                                             \
+    }
+
+    const uint32_t tl32 = (uint32_t)TL;
+    for (uint32_t s0 = 0u; s0 < tl32; s0 += 4u) {  // TL: kernel-uniform
+        BKD_STREAM_STEP(X0, W0, B0, s0)
+        BKD_STREAM_STEP(X1, W1, B1, s0 + 1u)
+        BKD_STREAM_STEP(X2, W2, B2, s0 + 2u)
+        BKD_STREAM_STEP(X3, W3, B3, s0 + 3u)
+    }
+#undef BKD_STREAM_STEP
+    if (live && !fresh) {  // the range ends inside entry i
+        const uint32_t reg = finish_lanes<8>(lds, c0, c1, c2, c3);
+        if (g == 0) {
+            if (from_start) sa.plast[r] = reg;
+            else sa.pfirst[r] = reg;
+        }
+    }
+}
+
+// 8-lane groups, one range each (grid = ngroups / 128 blocks). A stream longer than kStreamMaxTL
+// lines per range (only a batch of heavily overlapping huge entries) takes every entry whole, one
+// per group, and the combine then does nothing but the entries outside the stream.
+template <bool NT>
+__global__ void __launch_bounds__(kBlock) crc_stream_ranges_kernel(const uint8_t* __restrict__ base, uint64_t size,
+                                                                   const uint64_t* __restrict__ offsets,
+                                                                   const uint32_t* __restrict__ lengths,
+                                                                   const uint32_t* __restrict__ seeds, uint32_t seed_all,
+                                                                   uint64_t n, const uint32_t* __restrict__ tables,
+                                                                   uint32_t* __restrict__ out, uint32_t* __restrict__ err,
+                                                                   StreamArgs sa) {
+    using Gm = Geo<8>;
+    const uint64_t end = sa.shdr[0];
+    if (end == 0u || size == 0u) return;  // no entry in the stream: the combine does them all
+    __shared__ __attribute__((aligned(16))) uint32_t lds[Gm::kLdsWords];
+    stage_tables<8>(lds, tables);
+    const int lane = threadIdx.x & 63;
+    const uint32_t lanereg = ((uint32_t)(lane & 31) << 2) | (1u << 16);
+    const uint64_t ngroups = (uint64_t)gridDim.x * (kBlock / 8);
+    const uint64_t gid = (uint64_t)blockIdx.x * (kBlock / 8) + (uint64_t)(threadIdx.x / 8);
+    const uint64_t TL = stream_range_len(end, ngroups);
+    if (TL > sa.maxtl) {  // (kernel-uniform)
+        const IndexedSrc src{n, offsets, lengths, seeds, seed_all, size, out};
+        groups_loop<8, 2, NT>(lds, lanereg, lane & 7, base, src, n, gid, ngroups, err);
+        return;
+    }
+    stream_ranges_loop<NT>(lds, lanereg, lane & 7, base, size, sa, n, gid, TL, end, out);
+}
+
+// ---- the combine ----
+// One thread per entry: entries outside the stream (empty, out of range, a padded message under
+// 4 bytes) folded serially; an entry inside one range: pad product and inversion of its raw
+// register; a longer entry: its pieces joined, plast[t0], pfirst[t0 + 1 .. t1] (Horner with
+// X = x^(1024 TL), the last piece's weight x^(1024 L)), then x^(-8 pad). Entries of more than
+// kStreamSerialPieces pieces are joined by the whole block afterwards, one at a time.
+constexpr uint32_t kStreamSerialPieces = 64;
+
+__global__ void __launch_bounds__(1024, BKD_PLAN_OCC) stream_combine_kernel(
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ lengths,
+    const uint32_t* __restrict__ seeds, uint32_t seed_all, uint64_t size, uint64_t n, uint32_t nb,
+    const uint32_t* __restrict__ btab, const uint32_t* __restrict__ xinv, uint32_t poly, uint32_t x1024,
+    StreamArgs sa, uint32_t* __restrict__ out, uint32_t* __restrict__ err) {
+    __shared__ uint32_t T[16 * 256];  // slice-by-16 (serial entries)
+    __shared__ uint32_t big[1024];
+    __shared__ uint32_t nbig, sX;
+    __shared__ uint32_t red[1024 / 64];
+    const uint64_t end = sa.shdr[0];
+    const uint64_t TL = stream_range_len(end, sa.ngroups);
+    const bool whole = end != 0u && TL > sa.maxtl;  // the tile kernel took every entry whole
+    build_slice16(T, btab);
+    if (threadIdx.x == 0) sX = gf_pow_bits(x1024, (uint32_t)(TL < 0xFFFFFFFFu ? TL : 0u), poly);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *sa.ticket = 0u;  // plan_stream_kernel of this call is done
+    __syncthreads();
+    const uint32_t X = sX;
+    auto last_w = [&](uint64_t P1, uint64_t t1) { return gf_pow_bits(x1024, (uint32_t)(P1 - t1 * TL + 1u), poly); };
+    for (uint32_t eb = blockIdx.x; eb < nb; eb += gridDim.x) {
+        if (threadIdx.x == 0) nbig = 0u;
+        __syncthreads();
+        const uint64_t i = (uint64_t)eb * 1024u + threadIdx.x;
+        if (i < n && !whole) {
+            const uint64_t sp = sa.spos[i];
+            const uint64_t o = offsets[i];
+            const uint32_t l = lengths[i];
+            if (sp >> 63) {
+                if (!entry_valid(o, l, size)) {
+                    out[i] = 0u;
+                    if (err) atomicOr(err, 1u);
+                } else {
+                    const uint32_t reg = ~(seeds ? seeds[i] : seed_all);
+                    out[i] = l ? ~serial_crc(base, o, l, reg, T) : ~reg;
+                }
+            } else {
+                const SEnt e = stream_ent(o, l, size, sa.mis);
+                const uint64_t P0 = (sp & ((1ull << 62) - 1u)) - ((sp >> 62) & 1u), P1 = P0 + (e.Lst - e.F);
+                const uint64_t t0 = P0 / TL, t1 = P1 / TL, m = t1 - t0;
+                if (m == 0u) {
+                    const uint32_t raw = out[i];
+                    out[i] = ~(e.pad ? gf_mul_bits(xinv[e.pad], raw, poly) : raw);
+                } else if (m <= kStreamSerialPieces) {
+                    uint32_t reg = sa.plast[t0];
+                    for (uint64_t t = t0 + 1u; t < t1; ++t) reg = gf_mul_bits(X, reg, poly) ^ sa.pfirst[t];
+                    reg = gf_mul_bits(last_w(P1, t1), reg, poly) ^ sa.pfirst[t1];
+                    out[i] = ~(e.pad ? gf_mul_bits(xinv[e.pad], reg, poly) : reg);
+                } else {
+                    big[atomicAdd(&nbig, 1u)] = threadIdx.x;
+                }
+            }
+        }
+        __syncthreads();
+        const uint32_t nbg = nbig;
+        for (uint32_t k = 0; k < nbg; ++k) {  // block-uniform
+            const uint64_t ie = (uint64_t)eb * 1024u + big[k];
+            const SEnt e = stream_ent(offsets[ie], lengths[ie], size, sa.mis);
+            const uint64_t sp = sa.spos[ie];
+            const uint64_t P0 = (sp & ((1ull << 62) - 1u)) - ((sp >> 62) & 1u), P1 = P0 + (e.Lst - e.F);
+            const uint64_t t0 = P0 / TL, t1 = P1 / TL;
+            const uint32_t m = (uint32_t)(t1 - t0);  // pieces before the last: c = 0 .. m - 1, weight X^c
+            auto piece = [&](uint32_t c) { return c + 1u == m ? sa.plast[t0] : sa.pfirst[t1 - 1u - c]; };
+            const uint32_t per = (m + blockDim.x - 1u) / blockDim.x, lo = threadIdx.x * per,
+                           hi = lo + per < m ? lo + per : m;
+            uint32_t rr = 0u;
+            for (int c = (int)hi - 1; c >= (int)lo; --c) rr = gf_mul_bits(X, rr, poly) ^ piece((uint32_t)c);
+            if (lo < hi && lo) rr = gf_mul_bits(gf_pow_bits(X, lo, poly), rr, poly);
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) rr ^= (uint32_t)__shfl_xor((int)rr, d);
+            if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = rr;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                uint32_t reg = 0u;
+                for (uint32_t w = 0; w < blockDim.x / 64; ++w) reg ^= red[w];
+                reg = gf_mul_bits(last_w(P1, t1), reg, poly) ^ sa.pfirst[t1];
+                out[ie] = ~(e.pad ? gf_mul_bits(xinv[e.pad], reg, poly) : reg);
+            }
+            __syncthreads();
+        }
+    }
+}
+
+}  // namespace bkd

@@ -274,10 +274,11 @@ BKD_API uint32_t bkd_host_xpow8n(int algo, uint64_t nbytes);
 
 /* Tuning: lanes per entry group (0 = automatic, else 1/4/8/16/32/64); prefetch is fixed at build. */
 BKD_API int bkd_set_group_lanes(int lanes);
-/* Indexed-batch strategy: 0 = automatic (unless the base buffer is <= 256 KiB: the stream route when
- * the device finds the entries laid out in order (at most n/64 + 1 of them not continuing their
- * predecessor's lines), else the chunked plan), 1 = one entry per lane group, 2 = always the chunked
- * plan, 3 = always the stream route. */
+/* Indexed-batch strategy: 0 = automatic (one entry per lane group when the base buffer is <= 256 KiB;
+ * else the stream route (the entries' lines end to end, cut into one range per lane
+ * group; any index order) unless the buffer holds at most 1 KiB per entry, where the short-entry class
+ * and the chunked plan run), 1 = one entry per lane group, 2 = always the chunked plan, 3 = always the
+ * stream route (no short-entry class). Verify pipelines keep the chunked plan. */
 BKD_API int bkd_set_plan_mode(int mode);
 /* Chunked-plan geometry: lanes per group (4, 8, 16, 32 or 64), steps per full chunk (chunk = 16 * lanes *
  * steps bytes, <= 32 KiB) and the head-merge threshold in bytes (a head chunk shorter than this
@@ -298,6 +299,10 @@ BKD_API int bkd_set_plan_prefetch(int loads_in_flight);
  * 2 GHz), 1 = always the compiler's schedule, 2 = always the low-clock schedule
  * (16 table lookups in flight per step). Results are identical; only the speed differs. */
 BKD_API int bkd_set_fold_schedule(int schedule);
+/* Stream route: lines per range above which the range kernel takes every entry whole, one per lane
+ * group (only a batch of heavily overlapping huge entries reaches the default 2^22; tests lower it to
+ * exercise that path). >= 4. */
+BKD_API int bkd_set_stream_range_max(uint64_t lines);
 BKD_API int bkd_get_group_lanes(int algo, uint64_t mean_len);
 
 #ifdef __cplusplus

@@ -1,9 +1,10 @@
 """GPU: the stream route for ragged indexed batches (CPU model of the same
-decomposition: tests/stream_model.py) against the oracle, forced (plan mode 3) and automatic, on
-the layouts the index allows: packed (config 3's shape), packed with small gaps (framed payloads),
-unsorted, overlapping, empty and out-of-range entries, every base misalignment, tiles that end
-mid-entry, entries spanning one line, many tiles and more than 4096 tiles (the combine's wave and
-block paths). Reference arithmetic: circe crc32c() ($CN/cpp/crc32c_sse42.cpp:184-217) through the
+decomposition: tests/stream_model.py RangeModel) against the oracle, forced (plan mode 3) and
+automatic, on the layouts the index allows: packed (config 3's shape), packed with small gaps
+(framed payloads), unsorted, overlapping, empty and out-of-range entries, every base misalignment,
+runs of entries under a line (records outside the eight-entry window), ranges that end mid-entry,
+entries spanning more than 64 ranges (the combine's block path) and the whole-entry fallback of the
+range kernel. Reference arithmetic: circe crc32c() ($CN/cpp/crc32c_sse42.cpp:184-217) through the
 oracle, zlib for CRC32."""
 import numpy as np
 import pytest
@@ -20,6 +21,7 @@ def _reset():
     ck.set_plan_mode(0)
     yield
     ck.set_plan_mode(0)
+    ck.set_stream_range_max(1 << 22)
 
 
 def _run(gpu, data, offs, lens, seeds, algo, mis=0, mode=3):
@@ -104,7 +106,7 @@ def test_framed_payload_gaps(gpu, algo):
 
 @pytest.mark.parametrize("algo", [ck.CRC32C, ck.CRC32])
 def test_huge_entries_combine_paths(gpu, algo):
-    """Entries of > 64 tiles (wave combine) and > 4096 tiles (block combine) among small ones."""
+    """Entries spanning many ranges (more than 64: the combine's block path) among small ones."""
     rng = np.random.default_rng(9)
     lens = np.array([100, 64 * 4096 * 2 + 7, 50, 4096 * 4100 + 3, 1, 300, 4096 * 65, 4096 * 64, 4096 * 63 + 1, 77])
     offs = np.concatenate([[0], np.cumsum(lens[:-1])])
@@ -116,8 +118,8 @@ def test_huge_entries_combine_paths(gpu, algo):
 
 
 def test_stream_repeated_calls_same_stream(gpu):
-    """Route words and tile arrays are reused between calls on a stream: alternating packed (stream)
-    and unsorted (plan) batches through the automatic route stay exact."""
+    """The look-back words, ticket and range arrays are reused between calls on a stream: alternating
+    packed and permuted batches through the automatic route stay exact."""
     rng = np.random.default_rng(10)
     lens = rng.integers(1, 20000, 3000)
     offs = np.concatenate([[0], np.cumsum(lens[:-1])])
@@ -128,3 +130,38 @@ def test_stream_repeated_calls_same_stream(gpu):
         o, l, s = (offs, lens, seeds) if k % 2 == 0 else (offs[perm], lens[perm], seeds[perm])
         got = _run(gpu, data, o, l, s, ck.CRC32C, 0, 0)
         assert (got == _want(ck.CRC32C, data, o, l, s)).all(), k
+
+
+@pytest.mark.parametrize("algo", [ck.CRC32C, ck.CRC32])
+def test_whole_entry_fallback(gpu, algo):
+    """Ranges longer than the bound (lowered here from 2^22 lines): the range kernel takes every entry
+    whole, one per lane group, and the combine only the entries outside the stream."""
+    rng = np.random.default_rng(12)
+    lens = rng.choice([0, 1, 3, 64, 129, 4096, 100000], 3000)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1])])
+    offs[::11] += 5  # gaps: some entries past the end below
+    data = rng.bytes(int(lens.sum()))
+    seeds = rng.integers(0, 2**32, lens.size, dtype=np.uint64)
+    ck.set_stream_range_max(4)
+    got = _run(gpu, data, offs, lens, seeds, algo, 3, 3)
+    size = len(data)
+    want = [0 if offs[k] > size or lens[k] > size - offs[k] else
+            oracle.resume(algo, int(seeds[k]), data[offs[k]:offs[k] + lens[k]]) for k in range(lens.size)]
+    assert (got == np.array(want, dtype=np.uint32)).all()
+
+
+def test_tiny_entry_runs(gpu):
+    """Packed runs of 1..40-byte entries (more than eight entries begin within four lines: records
+    loaded outside the window) between long entries, at several misalignments."""
+    rng = np.random.default_rng(13)
+    parts = []
+    for k in range(300):
+        parts.append(rng.integers(1, 41, rng.integers(5, 60)))
+        parts.append(rng.integers(3000, 20000, 1))
+    lens = np.concatenate(parts)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1])])
+    data = rng.bytes(int(lens.sum()))
+    seeds = rng.integers(0, 2**32, lens.size, dtype=np.uint64)
+    for mis in (0, 45, 126):
+        got = _run(gpu, data, offs, lens, seeds, ck.CRC32C, mis, 3)
+        assert (got == _want(ck.CRC32C, data, offs, lens, seeds)).all(), mis
