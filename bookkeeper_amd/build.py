@@ -17,7 +17,7 @@ SOURCES = [os.path.join(CSRC, "bkdigest.hip")]
 # CPU route and host worker pool (plain C++, built with the host compiler)
 HOST_SOURCES = [os.path.join(CSRC, "host_crc.cpp"), os.path.join(CSRC, "host_batch.cpp")]
 DEPS = SOURCES + HOST_SOURCES + [os.path.join(CSRC, f) for f in (
-    "crc_kernels.hpp", "crc_tables.hpp", "plan_kernels.hpp", "host_crc.hpp", "host_batch.hpp")] + [os.path.join(ROOT, "include", "bkdigest.h")]
+    "crc_kernels.hpp", "crc_tables.hpp", "plan_kernels.hpp", "stream_kernels.hpp", "host_crc.hpp", "host_batch.hpp")] + [os.path.join(ROOT, "include", "bkdigest.h")]
 ARCH = os.environ.get("BKD_OFFLOAD_ARCH", "gfx950")
 
 

@@ -183,6 +183,7 @@ struct DeviceState {
     int cus = 0;
     uint32_t* tables[2][kNumLaneChoices] = {};  // [algo][lane choice] compact operator images
     uint32_t* xinv[2] = {};       // [algo] x^(-8k), k = 0..127: removes the plan's zero padding
+    uint32_t* xpw[2] = {};        // [algo] x^(1024 * 2^k), k = 0..63: the stream route's powers of a line
     std::shared_mutex maps_mu;    // guards xtab and scratch
     std::map<uint64_t, uint32_t*> xtab;  // (algo, CH) -> x^(8*CH) operator for the plan's combine
     std::map<hipStream_t, std::unique_ptr<StreamScratch>> scratch;
@@ -283,6 +284,11 @@ int init_device_locked(int dev) {
         for (uint32_t k = 0; k < 128; ++k) inv[k] = bkd::gf2::xpow_neg8(algo, k);
         BKD_HIP(hipMalloc(&ds.xinv[algo], sizeof(inv)));
         BKD_HIP(hipMemcpy(ds.xinv[algo], inv, sizeof(inv), hipMemcpyHostToDevice));
+        uint32_t pw[64];
+        pw[0] = bkd::gf2::xpow(algo, 1024);
+        for (int k = 1; k < 64; ++k) pw[k] = bkd::gf2::mul(algo, pw[k - 1], pw[k - 1]);
+        BKD_HIP(hipMalloc(&ds.xpw[algo], sizeof(pw)));
+        BKD_HIP(hipMemcpy(ds.xpw[algo], pw, sizeof(pw), hipMemcpyHostToDevice));
     }
     BKD_HIP(hipSetDevice(prev));
     ds.ready.store(true, std::memory_order_release);
@@ -465,7 +471,7 @@ int launch_stream(DeviceState& ds, int algo, const uint8_t* base, uint64_t size,
 #endif
     const uint32_t cgrid = std::min<uint32_t>(nb, (uint32_t)BKD_PLAN_GRID * (uint32_t)ds.cus);
     hipLaunchKernelGGL(bkd::stream_combine_kernel, dim3(cgrid), dim3(1024), 0, st, base, offsets, lengths, seeds, seed_all,
-                       size, n, nb, btab, ds.xinv[algo], bkd::gf2::poly(algo), bkd::gf2::xpow(algo, 1024), sa, out, err);
+                       size, n, nb, btab, ds.xinv[algo], bkd::gf2::poly(algo), ds.xpw[algo], sa, out, err);
     e = hipGetLastError();
     if (e != hipSuccess) return fail(BKD_ERR_HIP, std::string("stream kernels: ") + hipGetErrorString(e));
     return BKD_OK;
@@ -514,11 +520,11 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     const uint64_t capacity = std::min<uint64_t>(n + (size + 128u * n) / pg.ch + 16, 0xFFFFFFF0ull);
     const uint32_t nb = (uint32_t)((n + bkd::kPlanBlock - 1) / bkd::kPlanBlock);
     const uint32_t ncols = bkd::plan_ncols(pg);
-    // The stream route (stream_kernels.hpp): every ragged batch without a short class
-    // at the default geometry (8-lane groups; the tile kernel numbers device lines and entries in
-    // 32 bits); any index order, gaps or overlaps. Mode 2 keeps the chunked plan.
-    if (BKD_STREAM && (mode == 0 || mode == 3) && G == 8 && pg.small == 0u && size < (1ull << 38) &&
-        n < (1ull << 30) && !ext_flag)
+    // The stream route (stream_kernels.hpp, DESIGN.md §3 "Stream route"): plan mode 3, any index
+    // order, gaps or overlaps, at the default geometry (8-lane groups; the range kernel numbers
+    // device lines and entries in 32 bits). Not the automatic choice: on config 3 it measured
+    // 1.54 ms against the chunked plan's 1.16 ms (entry boundaries cost the whole wave).
+    if (BKD_STREAM && mode == 3 && G == 8 && size < (1ull << 38) && n < (1ull << 30) && !ext_flag)
         return launch_stream(ds, algo, base, size, offsets, lengths, n, seeds, seed_all, out, st, pg.mis);
     Carver cv;
     const size_t o_blk = cv.take((size_t)nb * ncols * 4), o_live = cv.take((size_t)nb * 4),

@@ -24,13 +24,16 @@ namespace bkd {
 #ifndef BKD_STREAM
 #define BKD_STREAM 1  // 0: ragged batches keep the chunked plan (A/B builds)
 #endif
+#ifndef BKD_STREAM_FINISH_PROBE
+#define BKD_STREAM_FINISH_PROBE 0  // 1: measurement-only build, an entry's finish is an XOR (wrong digests)
+#endif
 constexpr uint64_t kStreamMaxTL = 1ull << 22;  // lines per range (above: every entry whole, one per group)
 
 struct StreamArgs {
     uint64_t* sdesc;   // [nb] look-back words of the entry blocks: epoch | status | value
     uint64_t* shdr;    // [0] the stream's end (positions)
     uint64_t* spos;    // [n] V (first new line's position) | shared << 62 | outside the stream << 63
-    u32x4* srec;       // [n] {offset lo, offset hi, length, seed}
+    u32x4* srec;       // [n] the entry for the range kernel: {F, J, d | eL << 8 | in << 16, ~seed}
     uint32_t* pfirst;  // [ngroups] raw register of a range's first piece (its entry began before it)
     uint32_t* plast;   // [ngroups] raw register of a range's last piece (its entry goes on after it)
     uint32_t* ticket;  // entry-block ticket of plan_stream_kernel (0 between calls)
@@ -43,7 +46,7 @@ struct StreamArgs {
 __host__ __device__ __forceinline__ uint64_t stream_range_len(uint64_t end, uint64_t ngroups) {
     uint64_t tl = (end + ngroups - 1u) / ngroups;
     if (tl == 0u) tl = 1u;
-    return (tl + 3u) & ~3ull;  // a multiple of the tile loop's four line sets
+    return (tl + 7u) & ~7ull;  // a multiple of the range loop's body (two rounds of four line sets)
 }
 
 // Stream geometry of one entry (stream_model.Geo).
@@ -165,7 +168,12 @@ __global__ void __launch_bounds__(kPlanBlock) plan_stream_kernel(const uint64_t*
         if (i < n) {
             const uint64_t V = s_prefix + wpre + v - jn;
             sa.spos[i] = V | ((uint64_t)sh << 62) | ((uint64_t)!e.in << 63);
-            sa.srec[i] = u32x4{(uint32_t)o, (uint32_t)(o >> 32), l, seeds ? seeds[i] : seed_all};
+            // F: first device line, J: lines after it, d: its first byte in line F, eL: bytes of its last
+            // line it covers (1..128), in: in the stream
+            const uint32_t J = (uint32_t)(e.Lst - e.F), d = e.d;
+            const uint32_t eL = (uint32_t)((uint64_t)d + l - 128ull * J);
+            sa.srec[i] = u32x4{(uint32_t)e.F, J, d | ((eL & 0xFFu) << 8) | ((uint32_t)e.in << 16),
+                               ~(seeds ? seeds[i] : seed_all)};
         }
     }
 }
@@ -185,54 +193,70 @@ __device__ __forceinline__ u32x4 keep_range(u32x4 w, int32_t a, int32_t b) {
     return w;
 }
 
-// An entry's record decoded for the fold, relative to its range: byte 0 = the first byte of the
-// range's first position; its first line at position pF (may be negative: it began in an earlier
-// range). Bytes clamped to +-2^30 and positions to +-2^29 (an entry that far away never meets them).
-struct SRel {
-    int32_t a, e;    // first byte and end
-    int32_t sF, sL;  // positions of its first and last line
-    uint32_t d;      // bytes of its first line before it
-    uint32_t lst;    // device line of its last line
-    uint32_t F;      // device line of its first line
-    bool in;         // in the stream
+// An entry as the fold needs it, relative to its range (positions: the range's first line = 0; its
+// first line at pF, negative when it began in an earlier range; clamped to +-2^29, far enough): the
+// steps of its first and last line, and per lane the byte masks of those lines (the first line's
+// mask already ANDed with the last's for an entry of one line), the seed image (~seed XORed into
+// its first four bytes) and the seed's spill into the next line (d > 124). Computed once per entry
+// from its record (srec: F, J, d | eL << 8 | in << 16, ~seed) with 128-bit shifts.
+struct SFold {
+    int32_t sF, sL;
+    uint32_t lst;      // device line of its last line (the next entry shares it if it starts there)
+    u32x4 mA, mB;      // keep-masks of its first / last line
+    u32x4 simg;        // seed image in its first line
+    uint32_t spill;    // the seed image's bytes in the next line (lane 0, d > 124)
 };
 
-__device__ __forceinline__ SRel srel(const u32x4& r, int64_t pF, uint64_t size, uint32_t mis) {
-    const uint64_t o = (uint64_t)r.x | ((uint64_t)r.y << 32);
-    const uint32_t l = r.z;
-    const uint64_t as = (uint64_t)mis + o;
-    const uint64_t F = as >> 7, Lst = l ? (as + l - 1u) >> 7 : F;
-    SRel q;
-    q.d = (uint32_t)(as & 127u);
-    const int64_t A = pF * 128 + (int64_t)q.d, E = A + (int64_t)l, PL = pF + (int64_t)(Lst - F);
-    auto cl = [](int64_t v, int64_t m) -> int32_t { return (int32_t)(v < -m ? -m : (v > m ? m : v)); };
-    q.a = cl(A, 1 << 30);
-    q.e = cl(E, 1 << 30);
-    q.sF = cl(pF, 1 << 29);
-    q.sL = cl(PL, 1 << 29);
-    q.F = (uint32_t)F;
-    q.lst = (uint32_t)Lst;
-    const uint32_t pad = (128u - (uint32_t)((as + l) & 127u)) & 127u;
-    q.in = !(o > size || (uint64_t)l > size - o) && l != 0u && l + pad >= 4u;
-    return q;
+__device__ __forceinline__ u32x4 u128_from(uint64_t lo, uint64_t hi) {
+    return u32x4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+}
+// bytes [k, 16) of a 16-byte block set (k clamped to 0..16): all-ones << 8k
+__device__ __forceinline__ u32x4 mask_from(int32_t k) {
+    const uint32_t s = 8u * (uint32_t)(k < 0 ? 0 : (k > 16 ? 16 : k));
+    const uint64_t lo = s >= 64u ? 0ull : (~0ull << s);
+    const uint64_t hi = s >= 128u ? 0ull : (s >= 64u ? (~0ull << (s - 64u)) : ~0ull);
+    return u128_from(lo, hi);
+}
+// bytes [0, k) set (k clamped to 0..16): 2^(8k) - 1
+__device__ __forceinline__ u32x4 mask_below(int32_t k) {
+    const uint32_t b = 8u * (uint32_t)(k < 0 ? 0 : (k > 16 ? 16 : k));
+    const uint64_t lo = b == 0u ? 0ull : (b >= 64u ? ~0ull : (~0ull >> (64u - b)));
+    const uint64_t hi = b <= 64u ? 0ull : (~0ull >> (128u - b));
+    return u128_from(lo, hi);
 }
 
-// Device lines of a record: first, last, in the stream.
+__device__ __forceinline__ void sfold_setup(SFold& f, const u32x4& rq, int64_t pF, int g) {
+    const uint32_t J = rq.y, d = rq.z & 0xFFu, eL = (rq.z >> 8) & 0xFFu;
+    auto cl = [](int64_t v) -> int32_t { return (int32_t)(v < -(1 << 29) ? -(1 << 29) : (v > (1 << 29) ? (1 << 29) : v)); };
+    f.sF = cl(pF);
+    f.sL = cl(pF + (int64_t)J);
+    f.lst = rq.x + J;
+    const int32_t b = 16 * g;
+    f.mB = mask_below((int32_t)(eL == 0u ? 128u : eL) - b);
+    const u32x4 ma = mask_from((int32_t)d - b);
+    f.mA = J == 0u ? u32x4{ma.x & f.mB.x, ma.y & f.mB.y, ma.z & f.mB.z, ma.w & f.mB.w} : ma;
+    // the seed image: ~seed (rq.w) at byte d of the line, i.e. at byte x = d - 16 g of this lane's
+    // 16-byte block (x in -3 .. 15 touches it); bytes past the line go to the next line's lane 0
+    const int32_t x = (int32_t)d - b;
+    const uint64_t v = rq.w;
+    uint64_t lo = 0u, hi = 0u;
+    if (x >= 0 && x < 16) {
+        const uint32_t t = 8u * (uint32_t)x;
+        lo = t < 64u ? v << t : 0ull;
+        hi = t == 0u ? 0ull : (t < 64u ? v >> (64u - t) : v << (t - 64u));
+    } else if (x < 0 && x > -4) {
+        lo = v >> (uint32_t)(-8 * x);
+    }
+    f.simg = u128_from(lo, hi);
+    f.spill = (g == 0 && d > 124u) ? (uint32_t)(v >> (8u * (128u - d))) : 0u;
+}
+
+// The record's stream status, first and last device line.
 struct SLines {
     uint32_t F, Lst;
     bool in;
 };
-__device__ __forceinline__ SLines slines(const u32x4& r, uint64_t size, uint32_t mis) {
-    const uint64_t o = (uint64_t)r.x | ((uint64_t)r.y << 32);
-    const uint32_t l = r.z;
-    const uint64_t as = (uint64_t)mis + o;
-    SLines q;
-    q.F = (uint32_t)(as >> 7);
-    q.Lst = l ? (uint32_t)((as + l - 1u) >> 7) : q.F;
-    const uint32_t pad = (128u - (uint32_t)((as + l) & 127u)) & 127u;
-    q.in = !(o > size || (uint64_t)l > size - o) && l != 0u && l + pad >= 4u;
-    return q;
-}
+__device__ __forceinline__ SLines slines(const u32x4& r) { return SLines{r.x, r.x + r.y, ((r.z >> 16) & 1u) != 0u}; }
 
 // One range per 8-lane group. Four register sets hold the lines of the next four positions, loaded
 // by a cursor that walks the entries' records four positions ahead of the fold (the device line of
@@ -280,13 +304,14 @@ __device__ __forceinline__ void stream_ranges_loop(const uint32_t* lds, uint32_t
     const int64_t P0 = (int64_t)(sp0 & ((1ull << 62) - 1u)) - (int64_t)((sp0 >> 62) & 1u);  // its first line
     // fold state
     uint32_t i = j0;
-    SRel e = srel(rec0, P0 - (int64_t)R0, size, mis);
-    uint32_t r0 = ~rec0.w;
-    bool from_start = P0 >= (int64_t)R0, fresh = true, live = act, pin = true;
+    SFold f;
+    sfold_setup(f, rec0, P0 - (int64_t)R0, g);
+    const SLines q0 = slines(rec0);
+    bool from_start = P0 >= (int64_t)R0, live = act, pin = true;
     uint32_t c0 = 0u, c1 = 0u, c2 = 0u, c3 = 0u;
     // cursor: entry cj, device line cL of its position, crem new lines of cj after it, cpin: the
     // index before the next one looked at is in the stream
-    uint32_t cj = j0, cL = e.F + (uint32_t)((int64_t)R0 - P0), crem = e.lst - cL;
+    uint32_t cj = j0, cL = q0.F + (uint32_t)((int64_t)R0 - P0), crem = q0.Lst - cL;
     bool cpin = true;
     // the cursor's next position (records from window (WS, BS), or loaded on the spot)
     auto advance = [&](const u32x4& WS, uint32_t BS) {
@@ -314,7 +339,7 @@ __device__ __forceinline__ void stream_ranges_loop(const uint32_t* lds, uint32_t
                 asm volatile("s_waitcnt vmcnt(0)" : "+v"(rq.x), "+v"(rq.y), "+v"(rq.z), "+v"(rq.w));
             }
             cj = j;
-            const SLines q = slines(rq, size, mis);
+            const SLines q = slines(rq);
             if (!q.in) {
                 cpin = false;
                 continue;
@@ -328,114 +353,132 @@ __device__ __forceinline__ void stream_ranges_loop(const uint32_t* lds, uint32_t
         }
     };
     // prologue: the range's first four positions (records loaded on the spot: a window based past
-    // the end forces it)
+    // the end forces it), and the first round's record window
     const u32x4 none{0u, 0u, 0u, 0u};
-    u32x4 X0 = ld_line(cL), W0 = ld_rec(cj + 1u + (uint32_t)g);
-    uint32_t B0 = cj + 1u;
+    u32x4 WA = ld_rec(cj + 1u + (uint32_t)g), WB;
+    uint32_t BA = cj + 1u, BB;
+    u32x4 X0 = ld_line(cL);
     advance(none, 0xFFFFFFF0u);
-    u32x4 X1 = ld_line(cL), W1 = ld_rec(cj + 1u + (uint32_t)g);
-    uint32_t B1 = cj + 1u;
+    u32x4 X1 = ld_line(cL);
     advance(none, 0xFFFFFFF0u);
-    u32x4 X2 = ld_line(cL), W2 = ld_rec(cj + 1u + (uint32_t)g);
-    uint32_t B2 = cj + 1u;
+    u32x4 X2 = ld_line(cL);
     advance(none, 0xFFFFFFF0u);
-    u32x4 X3 = ld_line(cL), W3 = ld_rec(cj + 1u + (uint32_t)g);
-    uint32_t B3 = cj + 1u;
+    u32x4 X3 = ld_line(cL);
 
+    const u32x4 ones{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    // The next entry of the stream after i, from the window (WS, BS) or loaded on the spot (group-
+    // uniform): its fold setup at the position after `sv`, or at `sv` itself when it starts in the
+    // line where i ended (returns true then). live = false past the last entry.
+    auto next_entry = [&](const u32x4& WS, uint32_t BS, int32_t sv) -> bool {
+        const uint32_t plst = f.lst;
+        for (;;) {
+            ++i;
+            if (i >= n32) {
+                live = false;
+                return false;
+            }
+            const uint32_t k = i - BS;
+            u32x4 rq;
+            if (k < 8u) {
+                const int src = lane8 + (int)k;
+                rq.x = (uint32_t)__shfl((int)WS.x, src);
+                rq.y = (uint32_t)__shfl((int)WS.y, src);
+                rq.z = (uint32_t)__shfl((int)WS.z, src);
+                rq.w = (uint32_t)__shfl((int)WS.w, src);
+            } else {
+                rq = ld_rec(i);
+                asm volatile("s_waitcnt vmcnt(0)" : "+v"(rq.x), "+v"(rq.y), "+v"(rq.z), "+v"(rq.w));
+            }
+            const SLines q = slines(rq);
+            if (!q.in) {
+                pin = false;
+                continue;
+            }
+            const bool sh = pin && q.F == plst;
+            pin = true;
+            sfold_setup(f, rq, (int64_t)sv + (sh ? 0 : 1), g);
+            return sh;
+        }
+    };
+
+    // One step: position s of the range, line XS. The common path is masks by select and the fold;
+    // an entry that ends in this line takes the rare path (its finish, then every entry that starts
+    // in this same line: its first fold is the masked line itself, no product).
 #define BKD_STREAM_STEP(XS, WS, BS, S)                                                                \
     {                                                                                                 \
         const uint32_t s_ = (S);                                                                      \
-        const u32x4 w = XS;                                                                           \
-        bool more = live && s_ < nla;                                                                 \
-        while (__any(more)) {                                                                         \
-            if (more) {                                                                               \
-                const int32_t sv = (int32_t)s_;                                                       \
-                const int32_t lbase = 128 * sv + 16 * g;                                              \
-                u32x4 wm = w;                                                                         \
-                if (sv == e.sF || sv == e.sL) wm = keep_range(w, e.a - lbase, e.e - lbase);           \
-                if (sv == e.sF) {                                                                     \
-                    const int64_t dd = (int64_t)e.d - 16 * g;                                         \
-                    wm.x ^= place_seed(r0, dd);                                                       \
-                    wm.y ^= place_seed(r0, dd - 4);                                                   \
-                    wm.z ^= place_seed(r0, dd - 8);                                                   \
-                    wm.w ^= place_seed(r0, dd - 12);                                                  \
-                }                                                                                     \
-                if (sv == e.sF + 1 && e.d > 124u && g == 0) wm.x ^= place_seed(r0, (int64_t)e.d - 128); \
-                const uint32_t m0 = mul_main_add(lds, c0, lanereg, wm.x);                             \
-                const uint32_t m1 = mul_main_add(lds, c1, lanereg, wm.y);                             \
-                const uint32_t m2 = mul_main_add(lds, c2, lanereg, wm.z);                             \
-                const uint32_t m3 = mul_main_add(lds, c3, lanereg, wm.w);                             \
-                c0 = fresh ? wm.x : m0;                                                               \
-                c1 = fresh ? wm.y : m1;                                                               \
-                c2 = fresh ? wm.z : m2;                                                               \
-                c3 = fresh ? wm.w : m3;                                                               \
-                fresh = false;                                                                        \
-                more = false;                                                                         \
-                if (sv == e.sL) { /* the entry ends in this line: its raw register */                \
-                    const uint32_t reg = finish_lanes<8>(lds, c0, c1, c2, c3);                        \
+        const int32_t sv = (int32_t)s_;                                                               \
+        const bool act_ = live && s_ < nla;                                                           \
+        const bool first = sv == f.sF, last = sv == f.sL, spst = sv == f.sF + 1;                      \
+        if (__all(act_ && s_ + 1u < nla && !first && !last && !spst)) {                              \
+            /* wave-uniform fast path: every group inside an entry's inner lines */                  \
+            c0 = mul_main_add(lds, c0, lanereg, XS.x);                                                \
+            c1 = mul_main_add(lds, c1, lanereg, XS.y);                                                \
+            c2 = mul_main_add(lds, c2, lanereg, XS.z);                                                \
+            c3 = mul_main_add(lds, c3, lanereg, XS.w);                                                \
+        } else {                                                                                      \
+            /* the line masked to entry i's bytes, its seed image on its first line; c is 0 before */ \
+            /* an entry's first line, so its first fold is the masked line itself (a group past */   \
+            /* its last position folds garbage it never uses: the range's end was taken below) */    \
+            const u32x4 m = first ? f.mA : (last ? f.mB : ones);                                      \
+            c0 = mul_main_add(lds, c0, lanereg, (XS.x & m.x) ^ (first ? f.simg.x : (spst ? f.spill : 0u))); \
+            c1 = mul_main_add(lds, c1, lanereg, (XS.y & m.y) ^ (first ? f.simg.y : 0u));             \
+            c2 = mul_main_add(lds, c2, lanereg, (XS.z & m.z) ^ (first ? f.simg.z : 0u));             \
+            c3 = mul_main_add(lds, c3, lanereg, (XS.w & m.w) ^ (first ? f.simg.w : 0u));             \
+            if (act_ && last) { /* rare: entry i ends in this line */                                \
+                for (;;) {                                                                            \
+                    const uint32_t reg = BKD_STREAM_FINISH_PROBE ? (c0 ^ c1 ^ c2 ^ c3) : finish_lanes<8>(lds, c0, c1, c2, c3);                        \
                     if (g == 0) {                                                                     \
                         if (from_start) out[i] = reg;                                                 \
                         else sa.pfirst[r] = reg;                                                      \
                     }                                                                                 \
-                    fresh = true;                                                                     \
                     from_start = true;                                                                \
-                    const uint32_t plst = e.lst;                                                      \
-                    for (;;) { /* the next entry of the stream (group-uniform) */                    \
-                        ++i;                                                                          \
-                        if (i >= n32) {                                                               \
-                            live = false;                                                             \
-                            break;                                                                    \
-                        }                                                                             \
-                        const uint32_t k = i - BS;                                                    \
-                        u32x4 rq;                                                                     \
-                        if (k < 8u) {                                                                 \
-                            const int src = lane8 + (int)k;                                           \
-                            rq.x = (uint32_t)__shfl((int)WS.x, src);                                  \
-                            rq.y = (uint32_t)__shfl((int)WS.y, src);                                  \
-                            rq.z = (uint32_t)__shfl((int)WS.z, src);                                  \
-                            rq.w = (uint32_t)__shfl((int)WS.w, src);                                  \
-                        } else {                                                                      \
-                            rq = ld_rec(i);                                                           \
-                            asm volatile("s_waitcnt vmcnt(0)" : "+v"(rq.x), "+v"(rq.y), "+v"(rq.z), "+v"(rq.w)); \
-                        }                                                                             \
-                        const SLines q = slines(rq, size, mis);                                       \
-                        if (!q.in) {                                                                  \
-                            pin = false;                                                              \
-                            continue;                                                                 \
-                        }                                                                             \
-                        const bool sh = pin && q.F == plst;                                           \
-                        pin = true;                                                                   \
-                        e = srel(rq, (int64_t)sv + (sh ? 0 : 1), size, mis);                          \
-                        r0 = ~rq.w;                                                                   \
-                        more = sh; /* it starts in this same line */                                  \
-                        break;                                                                        \
-                    }                                                                                 \
+                    c0 = c1 = c2 = c3 = 0u;                                                           \
+                    if (!next_entry(WS, BS, sv)) break; /* it starts in the next line */             \
+                    /* it starts in this line: its first fold is the line masked, seed XORed in */   \
+                    c0 = (XS.x & f.mA.x) ^ f.simg.x;                                                  \
+                    c1 = (XS.y & f.mA.y) ^ f.simg.y;                                                  \
+                    c2 = (XS.z & f.mA.z) ^ f.simg.z;                                                  \
+                    c3 = (XS.w & f.mA.w) ^ f.simg.w;                                                  \
+                    if (f.sL != sv) break; /* and goes on into the next line */                       \
+                }                                                                                     \
+            }                                                                                         \
+            if (live && s_ + 1u == nla && f.sF <= sv) { /* the range ends inside entry i */          \
+                const uint32_t reg = BKD_STREAM_FINISH_PROBE ? (c0 ^ c1 ^ c2 ^ c3) : finish_lanes<8>(lds, c0, c1, c2, c3);                            \
+                if (g == 0) {                                                                         \
+                    if (from_start) sa.plast[r] = reg;                                                \
+                    else sa.pfirst[r] = reg;                                                          \
                 }                                                                                     \
             }                                                                                         \
         }                                                                                             \
-        /* the cursor moves to position s + 4 with this slot's window; then the slot is refilled: */ \
-        /* the window first, then the line (neither is waited for before its own use) */             \
-        advance(WS, BS);                                                                              \
-        BS = cj + 1u;                                                                                 \
-        WS = ld_rec(BS + (uint32_t)g);                                                                \
+        /* the cursor moves to position s + 4 (with this round's window) and the slot is refilled */ \
+        if (crem > 0u) {                                                                              \
+            ++cL;                                                                                     \
+            --crem;                                                                                   \
+        } else {                                                                                      \
+            advance(WS, BS);                                                                          \
+        }                                                                                             \
         XS = ld_line(cL);                                                                             \
     }
 
+    // Rounds of four steps, two per iteration (the record windows alternate without a copy): each
+    // round loads the next round's window (the eight records after the cursor's entry) first.
     const uint32_t tl32 = (uint32_t)TL;
-    for (uint32_t s0 = 0u; s0 < tl32; s0 += 4u) {  // TL: kernel-uniform
-        BKD_STREAM_STEP(X0, W0, B0, s0)
-        BKD_STREAM_STEP(X1, W1, B1, s0 + 1u)
-        BKD_STREAM_STEP(X2, W2, B2, s0 + 2u)
-        BKD_STREAM_STEP(X3, W3, B3, s0 + 3u)
+    for (uint32_t s0 = 0u; s0 < tl32; s0 += 8u) {  // TL: kernel-uniform, a multiple of 8
+        BB = cj + 1u;
+        WB = ld_rec(BB + (uint32_t)g);
+        BKD_STREAM_STEP(X0, WA, BA, s0)
+        BKD_STREAM_STEP(X1, WA, BA, s0 + 1u)
+        BKD_STREAM_STEP(X2, WA, BA, s0 + 2u)
+        BKD_STREAM_STEP(X3, WA, BA, s0 + 3u)
+        BA = cj + 1u;
+        WA = ld_rec(BA + (uint32_t)g);
+        BKD_STREAM_STEP(X0, WB, BB, s0 + 4u)
+        BKD_STREAM_STEP(X1, WB, BB, s0 + 5u)
+        BKD_STREAM_STEP(X2, WB, BB, s0 + 6u)
+        BKD_STREAM_STEP(X3, WB, BB, s0 + 7u)
     }
 #undef BKD_STREAM_STEP
-    if (live && !fresh) {  // the range ends inside entry i
-        const uint32_t reg = finish_lanes<8>(lds, c0, c1, c2, c3);
-        if (g == 0) {
-            if (from_start) sa.plast[r] = reg;
-            else sa.pfirst[r] = reg;
-        }
-    }
 }
 
 // 8-lane groups, one range each (grid = ngroups / 128 blocks). A stream longer than kStreamMaxTL
@@ -471,28 +514,43 @@ __global__ void __launch_bounds__(kBlock) crc_stream_ranges_kernel(const uint8_t
 // One thread per entry: entries outside the stream (empty, out of range, a padded message under
 // 4 bytes) folded serially; an entry inside one range: pad product and inversion of its raw
 // register; a longer entry: its pieces joined, plast[t0], pfirst[t0 + 1 .. t1] (Horner with
-// X = x^(1024 TL), the last piece's weight x^(1024 L)), then x^(-8 pad). Entries of more than
-// kStreamSerialPieces pieces are joined by the whole block afterwards, one at a time.
+// X = x^(1024 TL), the last piece's weight x^(1024 L)), then x^(-8 pad). Powers come from two
+// 64-entry tables in LDS, x^(1024 * 2^k) (xpw, from the host) and X^(2^k) (built from it for this
+// TL), so a power costs one product per set bit of its exponent. Entries of more than
+// kStreamSerialPieces pieces are joined afterwards by one wave each (lanes split the pieces).
 constexpr uint32_t kStreamSerialPieces = 64;
 
 __global__ void __launch_bounds__(1024, BKD_PLAN_OCC) stream_combine_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ lengths,
     const uint32_t* __restrict__ seeds, uint32_t seed_all, uint64_t size, uint64_t n, uint32_t nb,
-    const uint32_t* __restrict__ btab, const uint32_t* __restrict__ xinv, uint32_t poly, uint32_t x1024,
-    StreamArgs sa, uint32_t* __restrict__ out, uint32_t* __restrict__ err) {
+    const uint32_t* __restrict__ btab, const uint32_t* __restrict__ xinv, uint32_t poly,
+    const uint32_t* __restrict__ xpw, StreamArgs sa, uint32_t* __restrict__ out, uint32_t* __restrict__ err) {
     __shared__ uint32_t T[16 * 256];  // slice-by-16 (serial entries)
     __shared__ uint32_t big[1024];
-    __shared__ uint32_t nbig, sX;
-    __shared__ uint32_t red[1024 / 64];
+    __shared__ uint32_t pwL[64], pwX[64];
+    __shared__ uint32_t nbig;
     const uint64_t end = sa.shdr[0];
     const uint64_t TL = stream_range_len(end, sa.ngroups);
-    const bool whole = end != 0u && TL > sa.maxtl;  // the tile kernel took every entry whole
+    const bool whole = end != 0u && TL > sa.maxtl;  // the range kernel took every entry whole
     build_slice16(T, btab);
-    if (threadIdx.x == 0) sX = gf_pow_bits(x1024, (uint32_t)(TL < 0xFFFFFFFFu ? TL : 0u), poly);
     if (blockIdx.x == 0 && threadIdx.x == 0) *sa.ticket = 0u;  // plan_stream_kernel of this call is done
+    if (threadIdx.x < 64) pwL[threadIdx.x] = xpw[threadIdx.x];
     __syncthreads();
-    const uint32_t X = sX;
-    auto last_w = [&](uint64_t P1, uint64_t t1) { return gf_pow_bits(x1024, (uint32_t)(P1 - t1 * TL + 1u), poly); };
+    if (threadIdx.x < 64) {  // X^(2^k) = x^(1024 TL 2^k): one product per set bit of TL
+        const uint32_t k = threadIdx.x;
+        uint32_t r = 0x80000000u;  // x^0
+        for (uint32_t b = 0; b + k < 64u && b < 64u; ++b)
+            if ((TL >> b) & 1u) r = gf_mul_bits(r, pwL[b + k], poly);
+        pwX[k] = r;
+    }
+    __syncthreads();
+    auto pow_tab = [&](const uint32_t* pw, uint64_t e) {
+        uint32_t r = 0x80000000u;
+        for (uint32_t b = 0; e; ++b, e >>= 1)
+            if (e & 1u) r = gf_mul_bits(r, pw[b], poly);
+        return r;
+    };
+    const uint32_t X = pwX[0];
     for (uint32_t eb = blockIdx.x; eb < nb; eb += gridDim.x) {
         if (threadIdx.x == 0) nbig = 0u;
         __syncthreads();
@@ -519,7 +577,7 @@ __global__ void __launch_bounds__(1024, BKD_PLAN_OCC) stream_combine_kernel(
                 } else if (m <= kStreamSerialPieces) {
                     uint32_t reg = sa.plast[t0];
                     for (uint64_t t = t0 + 1u; t < t1; ++t) reg = gf_mul_bits(X, reg, poly) ^ sa.pfirst[t];
-                    reg = gf_mul_bits(last_w(P1, t1), reg, poly) ^ sa.pfirst[t1];
+                    reg = gf_mul_bits(pow_tab(pwL, P1 - t1 * TL + 1u), reg, poly) ^ sa.pfirst[t1];
                     out[i] = ~(e.pad ? gf_mul_bits(xinv[e.pad], reg, poly) : reg);
                 } else {
                     big[atomicAdd(&nbig, 1u)] = threadIdx.x;
@@ -527,8 +585,9 @@ __global__ void __launch_bounds__(1024, BKD_PLAN_OCC) stream_combine_kernel(
             }
         }
         __syncthreads();
-        const uint32_t nbg = nbig;
-        for (uint32_t k = 0; k < nbg; ++k) {  // block-uniform
+        // entries of many pieces: one wave each, the lanes' Horner runs placed by X^(run start)
+        const uint32_t nbg = nbig, lane = threadIdx.x & 63u, nwaves = blockDim.x >> 6;
+        for (uint32_t k = threadIdx.x >> 6; k < nbg; k += nwaves) {  // wave-uniform
             const uint64_t ie = (uint64_t)eb * 1024u + big[k];
             const SEnt e = stream_ent(offsets[ie], lengths[ie], size, sa.mis);
             const uint64_t sp = sa.spos[ie];
@@ -536,23 +595,18 @@ __global__ void __launch_bounds__(1024, BKD_PLAN_OCC) stream_combine_kernel(
             const uint64_t t0 = P0 / TL, t1 = P1 / TL;
             const uint32_t m = (uint32_t)(t1 - t0);  // pieces before the last: c = 0 .. m - 1, weight X^c
             auto piece = [&](uint32_t c) { return c + 1u == m ? sa.plast[t0] : sa.pfirst[t1 - 1u - c]; };
-            const uint32_t per = (m + blockDim.x - 1u) / blockDim.x, lo = threadIdx.x * per,
-                           hi = lo + per < m ? lo + per : m;
+            const uint32_t per = (m + 63u) >> 6, lo = lane * per, hi = lo + per < m ? lo + per : m;
             uint32_t rr = 0u;
             for (int c = (int)hi - 1; c >= (int)lo; --c) rr = gf_mul_bits(X, rr, poly) ^ piece((uint32_t)c);
-            if (lo < hi && lo) rr = gf_mul_bits(gf_pow_bits(X, lo, poly), rr, poly);
+            if (lo < hi && lo) rr = gf_mul_bits(pow_tab(pwX, lo), rr, poly);
 #pragma unroll
             for (int d = 1; d < 64; d <<= 1) rr ^= (uint32_t)__shfl_xor((int)rr, d);
-            if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = rr;
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                uint32_t reg = 0u;
-                for (uint32_t w = 0; w < blockDim.x / 64; ++w) reg ^= red[w];
-                reg = gf_mul_bits(last_w(P1, t1), reg, poly) ^ sa.pfirst[t1];
+            if (lane == 0u) {
+                const uint32_t reg = gf_mul_bits(pow_tab(pwL, P1 - t1 * TL + 1u), rr, poly) ^ sa.pfirst[t1];
                 out[ie] = ~(e.pad ? gf_mul_bits(xinv[e.pad], reg, poly) : reg);
             }
-            __syncthreads();
         }
+        __syncthreads();  // big[] and nbig are rebuilt by the next entry block
     }
 }
 

@@ -274,11 +274,11 @@ BKD_API uint32_t bkd_host_xpow8n(int algo, uint64_t nbytes);
 
 /* Tuning: lanes per entry group (0 = automatic, else 1/4/8/16/32/64); prefetch is fixed at build. */
 BKD_API int bkd_set_group_lanes(int lanes);
-/* Indexed-batch strategy: 0 = automatic (one entry per lane group when the base buffer is <= 256 KiB;
- * else the stream route (the entries' lines end to end, cut into one range per lane
- * group; any index order) unless the buffer holds at most 1 KiB per entry, where the short-entry class
- * and the chunked plan run), 1 = one entry per lane group, 2 = always the chunked plan, 3 = always the
- * stream route (no short-entry class). Verify pipelines keep the chunked plan. */
+/* Indexed-batch strategy: 0 = automatic (one entry per lane group when the base buffer is <= 256 KiB,
+ * else the chunked plan with the short-entry class when the buffer holds at most 1 KiB per entry),
+ * 1 = one entry per lane group, 2 = always the chunked plan, 3 = the stream route (the
+ * entries' lines end to end, one range of lines per lane group, any index order; no short-entry
+ * class). Verify pipelines keep the chunked plan. */
 BKD_API int bkd_set_plan_mode(int mode);
 /* Chunked-plan geometry: lanes per group (4, 8, 16, 32 or 64), steps per full chunk (chunk = 16 * lanes *
  * steps bytes, <= 32 KiB) and the head-merge threshold in bytes (a head chunk shorter than this

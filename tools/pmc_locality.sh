@@ -1,13 +1,13 @@
 #!/bin/bash
-# Instruction mix and stall counters of the CRC kernels per tools/ab_libs.py workload (one
-# rocprofv3 --pmc pass per counter set; AB_WORK names the workloads, the library is the in-tree one).
+# Address-translation and L2 counters of the stream route's range kernel against the chunk kernel on
+# the same workloads (tools/ab_libs.py; AB_MODE selects the route of the in-tree library).
 set -o pipefail
-R=${GRAFT_REPO_ROOT:-/root/repo}; O=$R/gpurun_out/pmcw${PMC_TAG}; mkdir -p $O
+R=${GRAFT_REPO_ROOT:-/root/repo}; O=$R/gpurun_out/pmcl${PMC_TAG}; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 i=0
-for C in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
-         "SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INST_LEVEL_VMEM SQ_WAVES GRBM_GUI_ACTIVE" \
-         "SQC_ICACHE_MISSES SQC_ICACHE_HITS SQ_IFETCH SQ_WAIT_INST_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"; do
+for C in "TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_STALL_MULTI_MISS_sum GRBM_GUI_ACTIVE" \
+         "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum GRBM_GUI_ACTIVE" \
+         "TCP_PENDING_STALL_CYCLES_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   for w in $AB_WORK; do
     AB_WORK=$w AB_ROUNDS=2 timeout -k 10 -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $O/p$i/$w -o p -- python3 $R/tools/ab_libs.py ${PMC_LIB:-$R/bookkeeper_amd/libbkdigest.so} > $O/p${i}_$w.log 2>&1 || { echo "fail $i $w"; tail -5 $O/p${i}_$w.log; exit 1; }
