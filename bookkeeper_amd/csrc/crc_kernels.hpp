@@ -1310,6 +1310,9 @@ __device__ __forceinline__ void long_chunks_loop(const uint32_t* lds, uint32_t l
 #define BKD_SHORT_PF 3
 #endif
 constexpr int kShortPF = BKD_SHORT_PF;
+#ifndef BKD_SHORT_NT
+#define BKD_SHORT_NT 0  // the short tail's loads are cached: heads share lines with their neighbours (1: nontemporal)
+#endif
 
 // The chunk list [0, n) (crc_plan_chunks_kernel): [0, nmain) by long_chunks_loop, then the short
 // tail [nmain, n) by short_chunks_loop (nmain == n: no short tail).
@@ -1320,7 +1323,8 @@ __device__ __forceinline__ void plan_chunks_loop(const uint32_t* lds, uint32_t l
                                                  uint32_t* __restrict__ out, uint32_t* __restrict__ partials) {
     if (gid < nmain) long_chunks_loop<G, PF, NT>(lds, lanereg, g, base, descs, nmain, gid, ngroups, out, partials);
     if (nmain < n && gid < n - nmain)
-        short_chunks_loop<G, kShortPF, NT>(lds, lanereg, g, base, descs, nmain + gid, n, ngroups, out, partials);
+        short_chunks_loop<G, kShortPF, NT && BKD_SHORT_NT>(lds, lanereg, g, base, descs, nmain + gid, n, ngroups, out,
+                                                          partials);
 }
 
 
