@@ -99,6 +99,9 @@ __device__ __forceinline__ uint32_t mul_main_add(const uint32_t* lds, uint32_t v
 #endif
 }
 
+#ifndef BKD_W0_CACHED
+#define BKD_W0_CACHED 0  // 1: every chunk's first block is a cached load (A/B)
+#endif
 #ifndef BKD_CLOCK_ADAPT
 #define BKD_CLOCK_ADAPT 1  // 0: the one-entry-per-group fold always uses mul_main_add
 #endif
@@ -973,7 +976,7 @@ __device__ __forceinline__ ChunkGeo chunk_geo(const PlanDesc& d, int g) {
 template <int G, int PF, bool NT>
 __device__ __forceinline__ void chunk_prefetch(const uint8_t* __restrict__ base, const ChunkGeo& c, u32x4& W0,
                                                u32x4 (&A)[PF]) {
-    W0 = ld16<NT>(base + c.la0);
+    W0 = ld16<NT && !BKD_W0_CACHED>(base + c.la0);  // a head's first line is its neighbour's last
 #pragma unroll
     for (int k = 0; k < PF; ++k) {
         const int64_t addr = (uint32_t)(k + 1) < c.J ? c.a + (int64_t)(k + 1) * Geo<G>::kStep : c.la0;
