@@ -82,6 +82,7 @@ PROTOTYPES = {
     "bkd_set_group_lanes": (_int, [_int]),
     "bkd_set_fold_schedule": (_int, [_int]),
     "bkd_set_stream_range_max": (_int, [_u64]),
+    "bkd_set_short_class_mean": (_int, [_u64]),
     "bkd_set_plan_mode": (_int, [_int]),
     "bkd_set_plan_geometry": (_int, [_int, _int, _int]),
     "bkd_set_plan_prefetch": (_int, [_int]),

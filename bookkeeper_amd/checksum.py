@@ -394,8 +394,14 @@ def set_stream_range_max(lines: int) -> None:
 
 
 def set_plan_small(max_bytes: int = 192) -> None:
-    """Entries of <= max_bytes of a planned indexed batch run in the short-entry launch (0 = none)."""
+    """Entries of <= max_bytes (<= 512) of a planned indexed batch run in the short-entry launch (0 = none)."""
     check(lib().bkd_set_plan_small(max_bytes))
+
+
+def set_short_class_mean(max_bytes_per_entry: int) -> None:
+    """The short-entry class runs when the base buffer holds at most this many bytes per entry
+    (default 1024; 2**64 - 1: whenever a bound is set)."""
+    check(lib().bkd_set_short_class_mean(max_bytes_per_entry))
 
 
 def set_plan_serial(max_bytes: int = 16) -> None:

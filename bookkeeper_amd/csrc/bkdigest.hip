@@ -205,8 +205,13 @@ std::atomic<int> g_plan_pf{2};  // loads in flight per lane in the chunk kernel 
 // Short-entry class of indexed batches: entries of <= this many bytes skip the plan and run in
 // their own launch (4-lane groups, next entry loaded during the current one). 0 = none.
 constexpr int kSmallLanes = 4;
-constexpr uint32_t kSmallMaxBytes = 16u * kSmallLanes * 3u;  // one register set per entry (PF = 2)
-std::atomic<uint32_t> g_plan_small{kSmallMaxBytes};
+constexpr uint32_t kSmallBytes4 = 16u * kSmallLanes * 3u;  // one register set per entry (4 lanes, PF = 2): 192 B
+#ifndef BKD_SMALL_WIDE
+#define BKD_SMALL_WIDE 8
+#endif
+constexpr int kSmallLanesWide = BKD_SMALL_WIDE;             // bounds above 192 B: 8 lanes, PF = 3 (16: 1 KiB)
+constexpr uint32_t kSmallMaxBytes = 16u * kSmallLanesWide * 4u;
+std::atomic<uint32_t> g_plan_small{kSmallBytes4};
 // Entries shorter than this skip the chunks: plan_combine computes them, one thread each. Longer
 // bounds cost more than they save on config 3's Zipf mix: 128 B took 36 us off the chunk kernel
 // and added 54 us to combine (random slice-by-16 lookups from 64 lanes conflict in LDS banks).
@@ -217,7 +222,7 @@ std::atomic<uint32_t> g_plan_serial{BKD_PLAN_SERIAL};
 #ifndef BKD_SHORT_MEAN_MAX
 #define BKD_SHORT_MEAN_MAX 1024
 #endif
-constexpr uint64_t kShortClassMeanMax = BKD_SHORT_MEAN_MAX;  // bytes of base buffer per entry
+std::atomic<uint64_t> g_short_mean_max{BKD_SHORT_MEAN_MAX};  // bytes of base buffer per entry (bkd_set_short_class_mean)
 #ifndef BKD_VERIFY_FUSED
 #define BKD_VERIFY_FUSED 1
 #endif
@@ -512,7 +517,8 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     // memory round trip each: it pays where short entries dominate (64 M x 64 B: 7.2 -> 1.9 ms) and
     // costs more than it saves where they are a minority of a large-entry batch (config 3's Zipf:
     // +54 us launch, -43 us chunk kernel). So it runs when the mean entry is at most 1 KiB.
-    pg.small = (short_class && size <= (uint64_t)kShortClassMeanMax * n) ? g_plan_small.load() : 0u;
+    const uint64_t mean_max = g_short_mean_max.load();
+    pg.small = (short_class && (mean_max == UINT64_MAX || size <= mean_max * n)) ? g_plan_small.load() : 0u;
     const uint32_t* xtab = nullptr;
     int rc = xtab_for(ds, algo, pg.ch, &xtab);
     if (rc) return rc;
@@ -561,10 +567,17 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     bkd::PlanDesc* descs = Carver::at<bkd::PlanDesc>(sb, o_desc);
     if (pg.small) {  // the short-entry class, in its own launch (any order against the plan kernels)
         const bkd::SmallIndexedSrc ss{n, offsets, lengths, seeds, seed_all, size, out, pg.small, run_word, run.epoch};
-        const uint64_t per_block = bkd::kBlock / kSmallLanes;
-        const unsigned sblocks = (unsigned)std::min<uint64_t>((n + per_block - 1) / per_block, (uint64_t)ds.cus);
-        hipLaunchKernelGGL((bkd::crc_groups_kernel<kSmallLanes, 2, kNT, bkd::SmallIndexedSrc>), dim3(sblocks),
-                           dim3(bkd::kBlock), 0, st, base, ss, ds.tables[algo][lane_index(kSmallLanes)], err, 1);
+        if (pg.small <= kSmallBytes4) {
+            const uint64_t per_block = bkd::kBlock / kSmallLanes;
+            const unsigned sblocks = (unsigned)std::min<uint64_t>((n + per_block - 1) / per_block, (uint64_t)ds.cus);
+            hipLaunchKernelGGL((bkd::crc_groups_kernel<kSmallLanes, 2, kNT, bkd::SmallIndexedSrc>), dim3(sblocks),
+                               dim3(bkd::kBlock), 0, st, base, ss, ds.tables[algo][lane_index(kSmallLanes)], err, 1);
+        } else {  // entries up to 1 KiB: 16-lane groups, an entry's four steps in one register set
+            const uint64_t per_block = bkd::kBlock / kSmallLanesWide;
+            const unsigned sblocks = (unsigned)std::min<uint64_t>((n + per_block - 1) / per_block, (uint64_t)ds.cus);
+            hipLaunchKernelGGL((bkd::crc_groups_kernel<kSmallLanesWide, 3, kNT, bkd::SmallIndexedSrc>), dim3(sblocks),
+                               dim3(bkd::kBlock), 0, st, base, ss, ds.tables[algo][lane_index(kSmallLanesWide)], err, 1);
+        }
     }
     // count / emit / combine walk their 1024-entry blocks in grid stride (BKD_PLAN_GRID blocks per CU;
     // 0: one block per entry block)
@@ -1316,6 +1329,11 @@ int bkd_set_plan_geometry(int lanes, int steps_per_chunk, int merge_bytes) {
     g_plan_lanes.store(lanes);
     g_plan_jc.store(steps_per_chunk);
     g_plan_merge.store(merge_bytes);
+    return BKD_OK;
+}
+
+int bkd_set_short_class_mean(uint64_t max_bytes_per_entry) {
+    g_short_mean_max.store(max_bytes_per_entry);
     return BKD_OK;
 }
 

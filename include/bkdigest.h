@@ -284,11 +284,15 @@ BKD_API int bkd_set_plan_mode(int mode);
  * steps bytes, <= 32 KiB) and the head-merge threshold in bytes (a head chunk shorter than this
  * joins its neighbour; >= 16). Default 8, 32, 16 (4 KiB chunks; tools/tune_plan.py). */
 BKD_API int bkd_set_plan_geometry(int lanes, int steps_per_chunk, int merge_bytes);
-/* Short-entry class of indexed batches that take the plan: entries of <= max_bytes (16..192; 0 = no
- * class) run in their own launch, 4-lane groups loading the next entry while folding the current
- * one, and skip the plan's count/emit/chunk/combine work. Used when the base buffer
- * holds at most 1 KiB per entry (short entries dominate). Default 192. */
+/* Short-entry class of indexed batches that take the plan: entries of <= max_bytes (16..512; 0 = no
+ * class) run in their own launch, loading the next entries while folding the current one (4-lane
+ * groups up to 192 B, 8-lane groups above), and skip the plan's count/emit/chunk/combine work
+ * (DESIGN.md §3). Used when the base buffer holds at most bkd_set_short_class_mean() bytes per entry
+ * (default 1 KiB: short entries dominate). Default 192. */
 BKD_API int bkd_set_plan_small(uint32_t max_bytes);
+/* The short-entry class's gate: base-buffer bytes per entry at most this (default 1024; UINT64_MAX:
+ * whenever a class bound is set). */
+BKD_API int bkd_set_short_class_mean(uint64_t max_bytes_per_entry);
 /* Entries of the plan shorter than `bytes` (16..64, default 16) skip the chunk kernel: the
  * combine kernel computes each with one thread (slice-by-16 over its 16-byte windows). */
 BKD_API int bkd_set_plan_serial(uint32_t bytes);

@@ -307,7 +307,7 @@ def test_package_batch_host_matches_oracle(gpu, algo, dtype, stride):
         assert bytes(frames[i, 32:32 + mac]) == oracle.digest_bytes(algo, d)
 
 
-@pytest.mark.parametrize("small", [0, 16, 100, 192])
+@pytest.mark.parametrize("small", [0, 16, 100, 192, 400, 512])
 def test_plan_short_entry_class(gpu, small):
     """Indexed batches through the plan with the short-entry class at several bounds: every length
     0..700 packed at odd offsets, seeded, plus out-of-range entries on both sides of the bound — the

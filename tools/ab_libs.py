@@ -36,6 +36,8 @@ def main(paths):
                 getattr(L, fn).argtypes = args
         if os.environ.get("AB_SMALL") and hasattr(L, "bkd_set_plan_small"):
             L.bkd_set_plan_small(int(os.environ["AB_SMALL"]))
+        if os.environ.get("AB_SHORT_MEAN") and hasattr(L, "bkd_set_short_class_mean"):
+            L.bkd_set_short_class_mean(int(os.environ["AB_SHORT_MEAN"]))
         if os.environ.get("AB_MODE") and hasattr(L, "bkd_set_plan_mode"):  # 0 auto, 1 direct, 2 plan, 3 stream
             L.bkd_set_plan_mode(int(os.environ["AB_MODE"]))
         if os.environ.get("AB_GEOM"):  # lanes,steps,merge for the plan (bkd_set_plan_geometry)
