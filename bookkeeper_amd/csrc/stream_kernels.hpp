@@ -36,7 +36,7 @@ struct StreamArgs {
     u32x4* srec;       // [n] the entry for the range kernel: {F, J, d | eL << 8 | in << 16, ~seed}
     uint32_t* pfirst;  // [ngroups] raw register of a range's first piece (its entry began before it)
     uint32_t* plast;   // [ngroups] raw register of a range's last piece (its entry goes on after it)
-    uint32_t* ticket;  // entry-block ticket of plan_stream_kernel (0 between calls)
+    uint32_t* ticket;  // entry-block ticket of plan_stream_kernel (0 between calls: its last block resets it)
     uint32_t ngroups;  // ranges = 8-lane groups of the tile kernel
     uint32_t mis;      // device address of base modulo 128
     uint32_t epoch;    // the call's epoch (look-back words of earlier calls never match)
@@ -89,7 +89,13 @@ __global__ void __launch_bounds__(kPlanBlock) plan_stream_kernel(const uint64_t*
     __shared__ uint32_t s_eb;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t ep = sa.epoch & 0xFFFFFu;
-    if (threadIdx.x == 0) s_eb = atomicAdd(sa.ticket, 1u);  // (stream_combine_kernel resets it)
+    if (threadIdx.x == 0) {
+        // one ticket per block; the block taking the last one resets the counter for the next call
+        // (a wrong start value could only misorder the blocks, never index past them)
+        const uint32_t t = atomicAdd(sa.ticket, 1u);
+        if (t == nb - 1u) __hip_atomic_store(sa.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_eb = t < nb ? t : t % nb;
+    }
     __syncthreads();
     {
         const uint32_t eb = s_eb;
@@ -533,7 +539,6 @@ __global__ void __launch_bounds__(1024, BKD_PLAN_OCC) stream_combine_kernel(
     const uint64_t TL = stream_range_len(end, sa.ngroups);
     const bool whole = end != 0u && TL > sa.maxtl;  // the range kernel took every entry whole
     build_slice16(T, btab);
-    if (blockIdx.x == 0 && threadIdx.x == 0) *sa.ticket = 0u;  // plan_stream_kernel of this call is done
     if (threadIdx.x < 64) pwL[threadIdx.x] = xpw[threadIdx.x];
     __syncthreads();
     if (threadIdx.x < 64) {  // X^(2^k) = x^(1024 TL 2^k): one product per set bit of TL
