@@ -1,25 +1,23 @@
-"""Pure-Python model of the stream route for ragged indexed batches (plan_kernels.hpp "stream"
-mode, crc_kernels.hpp stream_tiles_loop): the entries' 128-byte lines are laid end to end in index
-order (a line shared by an entry's end and the next entry's start counted once), cut into tiles of
-T lines, each tile folded by one lane group walking its entries line by line with byte masks; an
-entry that lies inside one tile gets its digest there, the pieces of longer entries are joined by
-the combine with x^(1024 L) per piece of L lines, then x^(-8 pad). Used on CPU to check the index
-arithmetic (positions, tiles, pieces, seed spill, pad) against the oracle before any GPU run.
+"""Pure-Python model of the stream route for ragged indexed batches (stream_kernels.hpp), used on
+CPU to check the index arithmetic against the oracle before any GPU run.
+
+The entries' 128-byte device lines are laid end to end in index order (a line shared by an entry's
+end and the next entry's start counted once); group r folds the positions [r TL, (r + 1) TL),
+TL = ceil(end / groups) rounded up to 8, with a cursor four positions ahead of the fold that walks
+the entries' records to find each position's device line; an entry inside one range gets its digest
+there, the pieces of longer entries are joined with x^(1024 TL) per range and x^(1024 L) for the
+last L lines, then x^(-8 pad).
 
 Geometry of entry i (a = device address modulo 128 + offset, `mis` = base address mod 128):
   as = mis + o, ae = as + l, first line F = as // 128, last line Lst = (ae - 1) // 128,
   d = as - 128 F (bytes before the entry in its first line), pad = 128 (Lst + 1) - ae.
 In the stream: valid, l >= 1 and l + pad >= 4 (the seed image must lie inside the padded message);
 others (empty, out of range) are done by the combine.
-  shared_i = entry i-1 in the stream and F_i == Lst_{i-1};  jump_i = not (F_i in {Lst_{i-1}, Lst_{i-1}+1})
-  start V_i = align_T(end_{i-1}) if jump_i else end_{i-1};  end_i = V_i + J_i - shared_i
-  (a jump starts a new tile, so the lines of every tile are consecutive device lines)
 """
 from __future__ import annotations
 
 import numpy as np
 
-T_LINES = 32
 
 
 class Geo:
@@ -35,39 +33,6 @@ class Geo:
         self.pad = 128 * (self.Lst + 1) - a_e
         self.as_, self.ae = a_s, a_e
         self.stream = self.valid and l >= 1 and l + self.pad >= 4
-
-
-def stream_layout(mis, offsets, lengths, size, tl=T_LINES):
-    n = len(offsets)
-    geo = [Geo(mis, int(offsets[i]), int(lengths[i]), size) for i in range(n)]
-    shared = [False] * n
-    jump = [False] * n
-    V = [0] * n
-    end = 0
-    for i, g in enumerate(geo):
-        if not g.stream:
-            continue
-        p = geo[i - 1] if i > 0 else None
-        if p is not None and p.stream:
-            shared[i] = g.F == p.Lst
-            jump[i] = not (g.F == p.Lst or g.F == p.Lst + 1)
-        else:
-            jump[i] = True
-        start = -(-end // tl) * tl if jump[i] else end
-        V[i] = start
-        end = start + g.J - int(shared[i])
-    ntiles = -(-end // tl)
-    tile_first = [-1] * ntiles
-    tile_k0 = [0] * ntiles
-    for i, g in enumerate(geo):
-        if not g.stream:
-            continue
-        P0 = V[i] - int(shared[i])
-        for p in range(V[i], V[i] + g.J - int(shared[i])):
-            if p % tl == 0:
-                tile_first[p // tl] = i
-                tile_k0[p // tl] = p - P0
-    return geo, shared, jump, V, end, tile_first, tile_k0
 
 
 class StreamModel:
@@ -89,110 +54,11 @@ class StreamModel:
             inv = (((inv ^ self.poly) << 1) | 1) & 0xFFFFFFFF if inv & 0x80000000 else (inv << 1) & 0xFFFFFFFF
         return inv
 
-    def digests(self, base: bytes, mis: int, offsets, lengths, seeds, foreign: bytes, tl=T_LINES):
-        """`base`: the caller's buffer; bytes of a line outside it come from `foreign` (stand-in for
-        whatever lies there) and must never change a digest."""
-        size = len(base)
-        geo, shared, jump, V, end, tile_first, tile_k0 = stream_layout(mis, offsets, lengths, size, tl)
-        n = len(geo)
-        out = [None] * n
-        pfirst, plast = {}, {}
 
-        def line_bytes(L):  # the 128 bytes of device line L (base index = 128 L - mis)
-            b0 = 128 * L - mis
-            return bytes(base[b0 + k] if 0 <= b0 + k < size else foreign[(b0 + k) % len(foreign)]
-                         for k in range(128))
-
-        def seed_image(i):
-            return (~int(seeds[i])) & 0xFFFFFFFF
-
-        for t in range(len(tile_first)):
-            i = tile_first[t]
-            assert i >= 0, t
-            g = geo[i]
-            LA = g.F + tile_k0[t]  # the tile's first device line
-            p = t * tl
-            piece = bytearray()
-            # the tile's first line is entry i's line k0: the piece starts at the entry's start iff k0 == 0
-            piece_from_start = tile_k0[t] == 0
-            L = LA
-            while p < min(t * tl + tl, end):
-                line = line_bytes(L)
-                while True:  # entries intersecting line L, in order
-                    g = geo[i]
-                    lo = max(g.as_, 128 * L) - 128 * L
-                    hi = min(g.ae, 128 * L + 128) - 128 * L
-                    m = bytearray(128)
-                    m[lo:hi] = line[lo:hi]
-                    if L == g.F:  # seed image at d (its spill, if any, lands in line F + 1)
-                        img = seed_image(i).to_bytes(4, "little")
-                        for k in range(4):
-                            if g.d + k < 128:
-                                m[g.d + k] ^= img[k]
-                    if L == g.F + 1 and g.d > 124:
-                        img = seed_image(i).to_bytes(4, "little")
-                        for k in range(4):
-                            if g.d + k >= 128:
-                                m[g.d + k - 128] ^= img[k]
-                    piece += m
-                    if L == g.Lst:  # the entry ends in this line
-                        reg = self.raw(bytes(piece))
-                        if piece_from_start:
-                            out[i] = (~self.gf_mul(reg, self.xinv8(g.pad))) & 0xFFFFFFFF
-                        else:
-                            pfirst[t] = reg
-                        piece = bytearray()
-                        piece_from_start = True
-                        nxt = i + 1
-                        if nxt >= n or not geo[nxt].stream or jump[nxt]:
-                            i = None
-                            break
-                        i = nxt
-                        if shared[i]:
-                            continue  # starts in this same line
-                        break
-                    break
-                if i is None:
-                    break
-                p += 1
-                L += 1
-                if p == t * tl + tl or p == end:  # the tile ends inside entry i (if it has begun)
-                    if not piece:
-                        break
-                    reg = self.raw(bytes(piece))
-                    P0 = V[i] - int(shared[i])
-                    if P0 < t * tl:
-                        pfirst[t] = reg
-                    else:
-                        plast[t] = reg
-                    break
-        # combine
-        for i, g in enumerate(geo):
-            if not g.stream:
-                if not g.valid:
-                    out[i] = 0
-                else:  # empty entry (or one whose padded message is < 4 bytes): serial
-                    out[i] = (~self.raw(bytes(base[g.o:g.o + g.l]), (~int(seeds[i])) & 0xFFFFFFFF)) & 0xFFFFFFFF
-                continue
-            P0 = V[i] - int(shared[i])
-            P1 = V[i] + g.J - int(shared[i]) - 1
-            t0, t1 = P0 // tl, P1 // tl
-            if t0 == t1:
-                assert out[i] is not None, i
-                continue
-            reg = plast[t0]
-            for t in range(t0 + 1, t1 + 1):
-                Lp = tl if t < t1 else P1 - tl * t1 + 1
-                reg = self.gf_mul(reg, self.xpow8n(128 * Lp)) ^ pfirst[t]
-            out[i] = (~self.gf_mul(reg, self.xinv8(g.pad))) & 0xFFFFFFFF
-        return out, {"end": end, "tiles": len(tile_first), "jumps": sum(jump), "shared": sum(shared)}
-
-
-# ---- round 4, second design: free jumps, one contiguous range of positions per group ----
-# An entry that does not continue its predecessor's lines no longer starts a new tile: it takes the
-# next position, and the group loads its lines from its own address (a cursor four positions ahead
-# of the fold walks the entries' records to find the device line of each position). Positions are a
-# plain prefix sum of the entries' new lines; group r folds positions [r TL, (r + 1) TL).
+# ---- positions and ranges ----
+# An entry takes the positions after its predecessor's whatever its address (gaps, unsorted,
+# overlapping); the group loads its lines from its own address. Positions are a plain prefix sum
+# of the entries' new lines.
 
 def range_layout(mis, offsets, lengths, size):
     """Per entry: Geo, shared (first line = the previous entry's last, both in the stream), V (its
@@ -213,7 +79,7 @@ def range_layout(mis, offsets, lengths, size):
     return geo, shared, V, Jn, end
 
 
-def range_geometry(end, groups, unroll=4):
+def range_geometry(end, groups, unroll=8):
     tl = -(-max(end, 1) // groups)
     tl = -(-tl // unroll) * unroll
     return tl, -(-end // tl)
@@ -222,7 +88,8 @@ def range_geometry(end, groups, unroll=4):
 class RangeModel(StreamModel):
     """The tile kernel of the free-jump design step by step: per group, a fold at position s and a
     cursor that walks entry records to load position s + 4's line; records come from 8-entry windows
-    loaded four steps ahead (`slow` counts the changes that needed a record outside the window)."""
+    loaded four steps ahead (`slow` counts the changes that needed a record outside the window; the
+    kernel loads one window per round of four steps, a round ahead)."""
 
     WIN = 8
 
