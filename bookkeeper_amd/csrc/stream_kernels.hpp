@@ -581,7 +581,14 @@ __global__ void __launch_bounds__(1024, BKD_PLAN_OCC) stream_combine_kernel(
                     out[i] = ~(e.pad ? gf_mul_bits(xinv[e.pad], raw, poly) : raw);
                 } else if (m <= kStreamSerialPieces) {
                     uint32_t reg = sa.plast[t0];
-                    for (uint64_t t = t0 + 1u; t < t1; ++t) reg = gf_mul_bits(X, reg, poly) ^ sa.pfirst[t];
+                    for (uint64_t t = t0 + 1u; t < t1; t += 8u) {  // pieces loaded eight at a time
+                        uint32_t pv[8];
+#pragma unroll
+                        for (int q = 0; q < 8; ++q) pv[q] = t + q < t1 ? sa.pfirst[t + q] : 0u;
+#pragma unroll
+                        for (int q = 0; q < 8; ++q)
+                            if (t + q < t1) reg = gf_mul_bits(X, reg, poly) ^ pv[q];
+                    }
                     reg = gf_mul_bits(pow_tab(pwL, P1 - t1 * TL + 1u), reg, poly) ^ sa.pfirst[t1];
                     out[i] = ~(e.pad ? gf_mul_bits(xinv[e.pad], reg, poly) : reg);
                 } else {
@@ -602,7 +609,16 @@ __global__ void __launch_bounds__(1024, BKD_PLAN_OCC) stream_combine_kernel(
             auto piece = [&](uint32_t c) { return c + 1u == m ? sa.plast[t0] : sa.pfirst[t1 - 1u - c]; };
             const uint32_t per = (m + 63u) >> 6, lo = lane * per, hi = lo + per < m ? lo + per : m;
             uint32_t rr = 0u;
-            for (int c = (int)hi - 1; c >= (int)lo; --c) rr = gf_mul_bits(X, rr, poly) ^ piece((uint32_t)c);
+            // pieces loaded eight at a time ahead of their products (one memory round trip per
+            // eight pieces instead of one per piece)
+            for (int c0 = (int)hi - 1; c0 >= (int)lo; c0 -= 8) {
+                uint32_t pv[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) pv[q] = c0 - q >= (int)lo ? piece((uint32_t)(c0 - q)) : 0u;
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    if (c0 - q >= (int)lo) rr = gf_mul_bits(X, rr, poly) ^ pv[q];
+            }
             if (lo < hi && lo) rr = gf_mul_bits(pow_tab(pwX, lo), rr, poly);
 #pragma unroll
             for (int d = 1; d < 64; d <<= 1) rr ^= (uint32_t)__shfl_xor((int)rr, d);

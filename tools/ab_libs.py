@@ -88,6 +88,8 @@ def main(paths):
         "indexed4k": (0, *idx(np.arange(n) * 4096, np.full(n, 4096)), n * 4096),
         # 16 entries of 256 MiB: the stream route's inner loop with almost no entry boundary
         "big16": (0, *idx(np.arange(16) * (n * 256), np.full(16, n * 256)), 16 * n * 256),
+        # 4096 entries of 1 MiB plus 7 bytes (unaligned ends), packed
+        "big1m": (0, *idx(np.arange(4096) * ((1 << 20) + 7), np.full(4096, (1 << 20) + 7)), 4096 * ((1 << 20) + 7)),
     }
 
     small = {f"u{S}_l{G}": (S, G) for S, G in ((32, 1), (32, 4), (64, 1), (64, 4), (64, 8), (128, 1), (128, 4),
