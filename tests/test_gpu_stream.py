@@ -165,3 +165,27 @@ def test_tiny_entry_runs(gpu):
     for mis in (0, 45, 126):
         got = _run(gpu, data, offs, lens, seeds, ck.CRC32C, mis, 3)
         assert (got == _want(ck.CRC32C, data, offs, lens, seeds)).all(), mis
+
+
+def test_many_entry_blocks_lookback(gpu):
+    """4M short entries (4096 entry blocks, many look-back windows of 64 blocks): the stream route
+    equals the chunked plan on every digest and the oracle on a sample."""
+    import torch
+    rng = np.random.default_rng(14)
+    n = 4 << 20
+    lens = rng.integers(1, 200, n)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1])])
+    size = int(offs[-1] + lens[-1])
+    base = torch.empty(size, dtype=torch.uint8, device=gpu)
+    ck.fill_splitmix64(base, 5)
+    d_off = torch.from_numpy(offs.astype(np.int64)).to(gpu)
+    d_len = torch.from_numpy(lens.astype(np.int32)).to(gpu)
+    got = {}
+    for mode in (3, 2):
+        ck.set_plan_mode(mode)
+        got[mode] = ck.crc_batch(ck.CRC32C, base, d_off, d_len).cpu().numpy().view(np.uint32)
+    assert (got[3] == got[2]).all()
+    host = base.cpu().numpy()
+    for k in rng.integers(0, n, 2000):
+        o, l = int(offs[k]), int(lens[k])
+        assert got[3][k] == oracle.resume(ck.CRC32C, 0, host[o:o + l].tobytes()), k
