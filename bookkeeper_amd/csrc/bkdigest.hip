@@ -300,7 +300,8 @@ int init_device_locked(int dev) {
     return BKD_OK;
 }
 
-// x^(8*ch) operator tables for the plan's combine, built once per (algo, ch) and device.
+// The plan combine's operators, built once per (algo, ch) and device (bkd::kXtab* layout):
+// tables of X = x^(8*ch), X^64 and X^1024, then X^L (L = 0..63) and X^(64 w) (w = 0..15).
 int xtab_for(DeviceState& ds, int algo, uint32_t ch, const uint32_t** out) {
     const uint64_t key = ((uint64_t)algo << 32) | ch;
     {
@@ -314,8 +315,12 @@ int xtab_for(DeviceState& ds, int algo, uint32_t ch, const uint32_t** out) {
     std::unique_lock<std::shared_mutex> wr(ds.maps_mu);
     auto it = ds.xtab.find(key);
     if (it == ds.xtab.end()) {
-        std::vector<uint32_t> xt(1024);
-        bkd::gf2::operator_tables(algo, bkd::gf2::xpow(algo, 8ull * ch), xt.data());
+        std::vector<uint32_t> xt(bkd::kXtabWords);
+        bkd::gf2::operator_tables(algo, bkd::gf2::xpow(algo, 8ull * ch), xt.data() + bkd::kXtabX);
+        bkd::gf2::operator_tables(algo, bkd::gf2::xpow(algo, 8ull * ch * 64u), xt.data() + bkd::kXtabX64);
+        bkd::gf2::operator_tables(algo, bkd::gf2::xpow(algo, 8ull * ch * 1024u), xt.data() + bkd::kXtabX1024);
+        for (uint32_t k = 0; k < 64u; ++k) xt[bkd::kXtabLane + k] = bkd::gf2::xpow(algo, 8ull * ch * k);
+        for (uint32_t k = 0; k < 16u; ++k) xt[bkd::kXtabWave + k] = bkd::gf2::xpow(algo, 8ull * ch * 64u * k);
         uint32_t* d = nullptr;
         BKD_HIP(hipMalloc(&d, xt.size() * sizeof(uint32_t)));
         BKD_HIP(hipMemcpy(d, xt.data(), xt.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
@@ -604,7 +609,7 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     }
     const uint32_t* btab = tab + bkd::gf2::byte_table_offset(G);
     hipLaunchKernelGGL(bkd::plan_combine_kernel, dim3(std::min(nb * reps, pgrid)), dim3(1024), 0, st, base, offsets, lengths, seeds,
-                       seed_all, size, n, pg, xtab, bkd::gf2::xpow(algo, 8ull * pg.ch), btab, ds.xinv[algo],
+                       seed_all, size, n, pg, xtab, btab, ds.xinv[algo],
                        bkd::gf2::poly(algo), pslot, hslot, partials, out, err, reps, blive, nb, run);
     e = hipGetLastError();
     if (e != hipSuccess) return fail(BKD_ERR_HIP, std::string("plan kernels: ") + hipGetErrorString(e));

@@ -448,11 +448,15 @@ __device__ __forceinline__ uint32_t gf_pow_bits(uint32_t x, uint32_t e, uint32_t
 // Horner over the partial registers of each chunked entry, then x^(-8*pad); serial fold of
 // entries the plan did not chunk. Entries with more than kCombineSerial chunks are combined by a
 // wave (up to kCombineWave chunks) or by the whole block (e.g. one 64 MiB entry = 16 Ki chunks)
-// instead of one serial thread: thread t folds its contiguous run of partials with Horner (table
-// X in LDS), is placed by X^(first chunk of its run) (bitwise power), and the wave or block
-// XOR-reduces.
+// instead of one serial thread: thread t of T (64 or 1024) folds chunks t, t + T, t + 2T, ... with
+// Horner by X^T (a wave's loads are consecutive partials), is placed by X^t (one bitwise product
+// per table word of t), and the wave or block XOR-reduces.
 constexpr uint32_t kCombineSerial = 64;
 constexpr uint32_t kCombineWave = 4096;
+// The combine's operator block (xtab_for): 4x256 tables of X = x^(8*CH), X^64 and X^1024, then the
+// words X^L (L = 0..63) and X^(64 w) (w = 0..15).
+constexpr uint32_t kXtabX = 0, kXtabX64 = 1024, kXtabX1024 = 2048, kXtabLane = 3072, kXtabWave = 3136;
+constexpr uint32_t kXtabWords = 3152;
 
 // Slice-by-16 tables in LDS: T[k * 256 + b] = byte b followed by k zero bytes; T[0 .. 255] is the
 // byte table. The reference's scalar fallback is the byte-at-a-time form of the same arithmetic
@@ -526,11 +530,31 @@ __device__ __forceinline__ uint32_t mul_x(const uint32_t* X, uint32_t r) {
     return xor3(X[r & 0xffu], X[256 + ((r >> 8) & 0xffu)], X[512 + ((r >> 16) & 0xffu)] ^ X[768 + (r >> 24)]);
 }
 
+// sum_j partial(t + T j) * (X^T)^j over the chunks t + T j < m of an entry (chunk m - 1, the head,
+// at hs; the rest at sl + c), by Horner from the highest j; the partials are loaded 8 at a time.
+template <uint32_t T>
+__device__ __forceinline__ uint32_t strided_horner(const uint32_t* XT, const uint32_t* __restrict__ partials,
+                                                   uint32_t sl, uint32_t hs, uint32_t m, uint32_t t) {
+    const int nj = t < m ? (int)((m - 1u - t) / T) + 1 : 0;
+    uint32_t r = 0u;
+    for (int j0 = nj - 1; j0 >= 0; j0 -= 8) {
+        uint32_t pv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t c = t + T * (uint32_t)(j0 - k);
+            pv[k] = j0 - k >= 0 ? partials[c + 1u == m ? hs : sl + c] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (j0 - k >= 0) r = mul_x(XT, r) ^ pv[k];
+    }
+    return r;
+}
+
 __global__ void __launch_bounds__(1024, BKD_PLAN_OCC) plan_combine_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ lengths,
     const uint32_t* __restrict__ seeds, uint32_t seed_all, uint64_t size, uint64_t n, PlanGeo pg,
-    const uint32_t* __restrict__ xtab, uint32_t xval,
-    const uint32_t* __restrict__ btab, const uint32_t* __restrict__ xinv, uint32_t poly,
+    const uint32_t* __restrict__ xtab, const uint32_t* __restrict__ btab, const uint32_t* __restrict__ xinv, uint32_t poly,
     const uint32_t* __restrict__ pslot, const uint32_t* __restrict__ hslot, const uint32_t* __restrict__ partials,
     uint32_t* __restrict__ out, uint32_t* __restrict__ err, uint32_t reps, const uint32_t* __restrict__ blive,
     uint32_t nblk, PlanRun run) {
@@ -539,13 +563,13 @@ __global__ void __launch_bounds__(1024, BKD_PLAN_OCC) plan_combine_kernel(
     // rest (invalid and serial entries are idempotent writes, cheap, and left to every replica).
     // Grid stride over the virtual blocks; the operator tables are staged once per block.
     if (!run.on()) return;
-    __shared__ uint32_t X[1024];
+    __shared__ uint32_t X[kXtabWords];  // xtab_for's operator block
     __shared__ uint32_t T[16 * 256];  // slice-by-16 (serial entries)
     __shared__ uint32_t big[1024];
     __shared__ uint32_t wsum[kPlanBlock / 64 + 1];
     __shared__ uint32_t nbig;
     __shared__ uint32_t red[1024 / 64];
-    for (int k = threadIdx.x; k < 1024; k += blockDim.x) X[k] = xtab[k];
+    for (int k = threadIdx.x; k < (int)kXtabWords; k += blockDim.x) X[k] = xtab[k];
     build_slice16(T, btab);
     const uint32_t nvb = nblk * reps;
     for (uint32_t vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
@@ -608,13 +632,8 @@ __global__ void __launch_bounds__(1024, BKD_PLAN_OCC) plan_combine_kernel(
         const EntryPlan p = plan_entry(offsets[e], lengths[e], size, pg);
         if (p.m > kCombineWave) continue;  // wave-uniform
         const uint32_t sl = pslot[e], hs = p.jh != pg.jc ? hslot[e] : sl + p.m - 1u;  // m > 64: full chunks exist
-        const uint32_t per = (p.m + 63u) >> 6;
-        const uint32_t lo = lane * per;
-        const uint32_t hi = lo + per < p.m ? lo + per : p.m;
-        uint32_t r = 0u;
-        for (int c = (int)hi - 1; c >= (int)lo; --c)
-            r = mul_x(X, r) ^ partials[(uint32_t)c + 1u == p.m ? hs : sl + (uint32_t)c];
-        if (lo < hi && lo) r = gf_mul_bits(gf_pow_bits(xval, lo, poly), r, poly);
+        uint32_t r = strided_horner<64u>(X + kXtabX64, partials, sl, hs, p.m, lane);
+        r = gf_mul_bits(X[kXtabLane + lane], r, poly);
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) r ^= (uint32_t)__shfl_xor((int)r, d);
         if (lane == 0u) out[e] = ~(p.pad ? gf_mul_bits(xinv[p.pad], r, poly) : r);
@@ -625,13 +644,9 @@ __global__ void __launch_bounds__(1024, BKD_PLAN_OCC) plan_combine_kernel(
         const EntryPlan p = plan_entry(offsets[e], lengths[e], size, pg);
         if (p.m <= kCombineWave) continue;  // block-uniform
         const uint32_t sl = pslot[e], hs = p.jh != pg.jc ? hslot[e] : sl + p.m - 1u;
-        const uint32_t per = (p.m + blockDim.x - 1u) / blockDim.x;
-        const uint32_t lo = threadIdx.x * per;
-        const uint32_t hi = lo + per < p.m ? lo + per : p.m;
-        uint32_t r = 0u;
-        for (int c = (int)hi - 1; c >= (int)lo; --c)
-            r = mul_x(X, r) ^ partials[(uint32_t)c + 1u == p.m ? hs : sl + (uint32_t)c];
-        if (lo < hi && lo) r = gf_mul_bits(gf_pow_bits(xval, lo, poly), r, poly);
+        uint32_t r = strided_horner<1024u>(X + kXtabX1024, partials, sl, hs, p.m, threadIdx.x);
+        r = gf_mul_bits(X[kXtabLane + lane], r, poly);  // X^t = X^lane * X^(64 wave)
+        r = gf_mul_bits(X[kXtabWave + (threadIdx.x >> 6)], r, poly);
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) r ^= (uint32_t)__shfl_xor((int)r, d);
         if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = r;
