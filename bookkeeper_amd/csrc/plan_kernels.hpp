@@ -190,10 +190,13 @@ __global__ void __launch_bounds__(kPlanBlock) plan_count_kernel(const uint64_t* 
     bool ok = true;  // length within the band of the reference (PlanRun::in_band)
     if (i < n) {
         const uint32_t l = lengths[i];
+        // without a short class every offset is needed: loaded beside its length (one round trip);
+        // with one, only for the plan's own entries (a batch of short entries reads no offsets)
+        const uint64_t o0 = pg.small == 0u ? offsets[i] : 0u;
         ok = PlanRun::in_band(l, ref);
-        if (!is_small(l, pg)) {  // offsets are read only for the plan's own entries
+        if (!is_small(l, pg)) {
             mine = 1u;
-            const EntryPlan p = plan_entry(offsets[i], l, size, pg);
+            const EntryPlan p = plan_entry(pg.small == 0u ? o0 : offsets[i], l, size, pg);
             if (p.kind == 0) {
                 if (p.jh != pg.jc) atomicAdd(&col[p.jh], 1u);
                 full = p.full;
@@ -325,13 +328,18 @@ __global__ void __launch_bounds__(kPlanBlock, BKD_PLAN_OCC) plan_emit_kernel(con
     const uint32_t nvb = nb * reps;
     for (uint32_t vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
     const uint32_t eb = vb / reps, rep = vb - eb * reps;
+    // the entry's index words, the live count and the cursors requested together (one round trip)
+    const uint64_t i = (uint64_t)eb * kPlanBlock + threadIdx.x;
+    const uint64_t ic = i < n ? i : n - 1u;
+    const uint64_t o = offsets[ic];
+    const uint32_t l = lengths[ic];
+    const uint32_t seed = seeds ? seeds[ic] : seed_all;
     if (blive[eb] == 0u) continue;  // only short entries (block-uniform)
     for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) cursor[k] = bin0[k] + blkoff[(uint64_t)k * nb + eb];
     __syncthreads();
-    const uint64_t i = (uint64_t)eb * kPlanBlock + threadIdx.x;
     EntryPlan p{};
     p.kind = 1;
-    if (i < n) p = plan_entry(offsets[i], lengths[i], size, pg);
+    if (i < n) p = plan_entry(o, l, size, pg);
     const bool chunked = i < n && p.kind == 0;
     uint32_t t_full;
     const uint32_t ex_full = block_excl_scan(chunked ? p.full : 0u, wsum, t_full);
@@ -344,7 +352,6 @@ __global__ void __launch_bounds__(kPlanBlock, BKD_PLAN_OCC) plan_emit_kernel(con
         const bool has_head = p.jh != pg.jc;
         const uint32_t hpos = has_head ? atomicAdd(&cursor[p.jh], 1u) : 0u;
         const bool overflow = ((uint64_t)rs + p.full > capacity) || (has_head && (uint64_t)hpos >= capacity);
-        const uint32_t seed = seeds ? seeds[i] : seed_all;
         // a chunk's partial goes to partials[its list position]: a wave's groups hold consecutive
         // positions, so their partials are one coalesced write (entry-ordered slots made every
         // partial a lone 4-byte write). pslot: the full run's first position, or the head's
@@ -574,20 +581,27 @@ __global__ void __launch_bounds__(1024, BKD_PLAN_OCC) plan_combine_kernel(
     const uint32_t nvb = nblk * reps;
     for (uint32_t vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
     const uint32_t eb = vb / reps, rep = vb - eb * reps;
-    if (blive[eb] == 0u) continue;  // only short entries: the short-entry launch wrote them
+    // every index word of the entry is requested at once, with the block's live count: one round
+    // trip before the partials (a word the entry turns out not to need costs nothing further)
+    const uint64_t i = (uint64_t)eb * blockDim.x + threadIdx.x;
+    const uint64_t ic = i < n ? i : n - 1u;
+    const uint32_t live = blive[eb];
+    uint32_t slot = pslot[ic];
+    const uint32_t hs_i = hslot[ic];
+    const uint64_t o = offsets[ic];
+    const uint32_t l = lengths[ic];
+    const uint32_t seed_i = seeds ? seeds[ic] : seed_all;
+    if (i >= n) slot = kNoSlot;
+    if (live == 0u) continue;  // only short entries: the short-entry launch wrote them
     if (threadIdx.x == 0) nbig = 0u;
     __syncthreads();
-    const uint64_t i = (uint64_t)eb * blockDim.x + threadIdx.x;
     uint32_t is_big = 0u;
-    const uint32_t slot = i < n ? pslot[i] : kNoSlot;
     if (slot != kNoSlot && slot != kDirect && slot != kSmall) {
-        const uint64_t o = offsets[i];
-        const uint32_t l = lengths[i];
         if (!entry_valid(o, l, size)) {
             out[i] = 0u;
             if (err) atomicOr(err, 1u);
         } else if (slot == kSerial) {
-            const uint32_t reg = ~(seeds ? seeds[i] : seed_all);
+            const uint32_t reg = ~seed_i;
             out[i] = l ? ~serial_crc(base, o, l, reg, T) : ~reg;
         } else {
             const EntryPlan p = plan_entry(o, l, size, pg);
@@ -598,7 +612,7 @@ __global__ void __launch_bounds__(1024, BKD_PLAN_OCC) plan_combine_kernel(
                 // partials in batches of 8 independent loads, then Horner from the head (chunk m - 1:
                 // at hslot when it is a separate head beside full chunks, else in the full run)
                 const bool sep = p.jh != pg.jc && p.full != 0u;
-                uint32_t reg = partials[sep ? hslot[i] : slot + p.m - 1u];
+                uint32_t reg = partials[sep ? hs_i : slot + p.m - 1u];
                 for (int c0 = (int)p.m - 2; c0 >= 0; c0 -= 8) {
                     uint32_t pv[8];
 #pragma unroll
