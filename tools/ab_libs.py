@@ -42,6 +42,8 @@ def main(paths):
             L.bkd_set_plan_mode(int(os.environ["AB_MODE"]))
         if os.environ.get("AB_LANES"):  # lanes per group of the one-entry-per-group kernels
             assert L.bkd_set_group_lanes(int(os.environ["AB_LANES"])) == 0
+        if os.environ.get("AB_PF"):  # loads in flight per lane in the chunk kernel (bkd_set_plan_prefetch)
+            assert L.bkd_set_plan_prefetch(int(os.environ["AB_PF"])) == 0
         if os.environ.get("AB_GEOM"):  # lanes,steps,merge for the plan (bkd_set_plan_geometry)
             assert L.bkd_set_plan_geometry(*(int(v) for v in os.environ["AB_GEOM"].split(","))) == 0
         libs[os.path.basename(p)] = L
