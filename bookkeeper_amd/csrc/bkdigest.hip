@@ -76,6 +76,38 @@ struct StreamScratch {
     uint32_t* uni = nullptr;  // PlanRun uniform-lengths word (the epoch of the call it holds for)
     uint32_t* ticket = nullptr;  // the stream route's entry-block ticket (StreamArgs::ticket), 0 between calls
     uint32_t epoch = 0;
+    // Decoupled look-back words (the stream route's positions): a region that holds nothing else, so
+    // a word not yet written by this call holds zero or an earlier call's word, never other data.
+    // Each call tags its words with the low bits of lb_calls (bkd::kLbEpochMask); the region is zeroed
+    // when allocated and whenever those bits wrap, so no earlier word can carry this call's tag.
+    uint64_t* lb = nullptr;
+    size_t lb_cap = 0;  // words
+    uint64_t lb_calls = 0;
+    hipError_t lookback_words(hipStream_t st, size_t words, uint32_t* tag, uint64_t** out) {
+        bool zero = false;
+        if (lb_cap < words) {
+            if (lb) {  // work already enqueued on this stream may still use the old region
+                const hipError_t e = hipStreamSynchronize(st);
+                if (e != hipSuccess) return e;
+                (void)hipFree(lb);
+            }
+            lb = nullptr;
+            lb_cap = 0;
+            const size_t want = words + words / 4 + 64;
+            hipError_t e = hipMalloc((void**)&lb, want * sizeof(uint64_t));
+            if (e != hipSuccess) return e;
+            lb_cap = want;
+            zero = true;
+        }
+        ++lb_calls;
+        *tag = (uint32_t)(lb_calls & bkd::kLbEpochMask);
+        if (zero || *tag == 0u) {
+            const hipError_t e = hipMemsetAsync(lb, 0, lb_cap * sizeof(uint64_t), st);
+            if (e != hipSuccess) return e;
+        }
+        *out = lb;
+        return hipSuccess;
+    }
     hipError_t ticket_word(hipStream_t st, uint32_t** out) {
         if (!ticket) {
             hipError_t e = hipMalloc((void**)&ticket, sizeof(uint32_t));
@@ -445,7 +477,7 @@ int launch_stream(DeviceState& ds, int algo, const uint8_t* base, uint64_t size,
     const uint32_t nb = (uint32_t)((n + bkd::kPlanBlock - 1) / bkd::kPlanBlock);
     const uint32_t ngroups = (uint32_t)ds.cus * (uint32_t)(bkd::kBlock / 8);
     Carver cv;
-    const size_t o_desc = cv.take((size_t)nb * 8), o_hdr = cv.take(64), o_pos = cv.take((size_t)n * 8),
+    const size_t o_hdr = cv.take(64), o_pos = cv.take((size_t)n * 8),
                  o_rec = cv.take((size_t)n * 16), o_pf = cv.take((size_t)ngroups * 4),
                  o_pl = cv.take((size_t)ngroups * 4);
     StreamScratch& sc = scratch_for(ds, st);
@@ -453,13 +485,15 @@ int launch_stream(DeviceState& ds, int algo, const uint8_t* base, uint64_t size,
     uint8_t* sb = nullptr;
     uint32_t* err = nullptr;
     uint32_t* ticket = nullptr;
+    uint64_t* lbw = nullptr;
+    uint32_t tag = 0;
     hipError_t e = sc.get(0, cv.used, st, &sb);
     if (e == hipSuccess) e = sc.flag(st, &err);
     if (e == hipSuccess) e = sc.ticket_word(st, &ticket);
+    if (e == hipSuccess) e = sc.lookback_words(st, nb, &tag, &lbw);
     if (e != hipSuccess) return fail(BKD_ERR_NOMEM, std::string("stream scratch: ") + hipGetErrorString(e));
-    if (++sc.epoch == 0u) ++sc.epoch;
     bkd::StreamArgs sa{};
-    sa.sdesc = Carver::at<uint64_t>(sb, o_desc);
+    sa.sdesc = lbw;
     sa.shdr = Carver::at<uint64_t>(sb, o_hdr);
     sa.spos = Carver::at<uint64_t>(sb, o_pos);
     sa.srec = Carver::at<bkd::u32x4>(sb, o_rec);
@@ -468,7 +502,7 @@ int launch_stream(DeviceState& ds, int algo, const uint8_t* base, uint64_t size,
     sa.ticket = ticket;
     sa.ngroups = ngroups;
     sa.mis = mis;
-    sa.epoch = sc.epoch;
+    sa.epoch = tag;
     sa.maxtl = g_stream_max_tl.load();
     const uint32_t* tab = ds.tables[algo][lane_index(8)];
     const uint32_t* btab = tab + bkd::gf2::byte_table_offset(8);
@@ -1456,6 +1490,7 @@ int bkd_stream_release(void* stream) {
             if (sc->buf[k]) BKD_HIP(hipFree(sc->buf[k]));
         for (uint32_t* w : {sc->err, sc->run, sc->uni, sc->vflag, sc->ticket})
             if (w) BKD_HIP(hipFree(w));
+        if (sc->lb) BKD_HIP(hipFree(sc->lb));
         if (sc->h_err) BKD_HIP(hipHostFree(sc->h_err));
     }
     return status;

@@ -27,10 +27,11 @@ namespace bkd {
 #ifndef BKD_STREAM_FINISH_PROBE
 #define BKD_STREAM_FINISH_PROBE 0  // 1: measurement-only build, an entry's finish is an XOR (wrong digests)
 #endif
+constexpr uint32_t kLbEpochMask = (1u << 22) - 1u;  // tag bits of a look-back word (StreamScratch::lookback_words)
 constexpr uint64_t kStreamMaxTL = 1ull << 22;  // lines per range (above: every entry whole, one per group)
 
 struct StreamArgs {
-    uint64_t* sdesc;   // [nb] look-back words of the entry blocks: epoch | status | value
+    uint64_t* sdesc;   // [nb] look-back words of the entry blocks: tag | status | value (a region of their own)
     uint64_t* shdr;    // [0] the stream's end (positions)
     uint64_t* spos;    // [n] V (first new line's position) | shared << 62 | outside the stream << 63
     u32x4* srec;       // [n] the entry for the range kernel: {F, J, d | eL << 8 | in << 16, ~seed}
@@ -39,7 +40,7 @@ struct StreamArgs {
     uint32_t* ticket;  // entry-block ticket of plan_stream_kernel (0 between calls: its last block resets it)
     uint32_t ngroups;  // ranges = 8-lane groups of the tile kernel
     uint32_t mis;      // device address of base modulo 128
-    uint32_t epoch;    // the call's epoch (look-back words of earlier calls never match)
+    uint32_t epoch;    // the call's look-back tag (words of earlier calls never carry it)
     uint64_t maxtl;    // lines per range above which every entry is taken whole (kStreamMaxTL; tests lower it)
 };
 
@@ -68,10 +69,14 @@ __device__ __forceinline__ SEnt stream_ent(uint64_t o, uint32_t l, uint64_t size
 }
 
 // ---- positions: plan_stream_kernel ----
-// look-back word: epoch (20 bits) | status (2: 1 = block aggregate, 2 = inclusive prefix) | value (42)
+// look-back word: tag (22 bits, the call's kLbEpochMask bits) | status (2: 1 = block aggregate,
+// 2 = inclusive prefix; 0 = not written) | value (40 bits: a prefix of lines, < 2^31 below 2^38 bytes)
 __device__ __forceinline__ uint64_t sd_pack(uint32_t epoch, uint32_t st, uint64_t v) {
-    return ((uint64_t)(epoch & 0xFFFFFu) << 44) | ((uint64_t)st << 42) | (v & ((1ull << 42) - 1u));
+    return ((uint64_t)(epoch & kLbEpochMask) << 42) | ((uint64_t)st << 40) | (v & ((1ull << 40) - 1u));
 }
+__device__ __forceinline__ uint32_t sd_tag(uint64_t w) { return (uint32_t)(w >> 42); }
+__device__ __forceinline__ uint32_t sd_status(uint64_t w) { return (uint32_t)(w >> 40) & 3u; }
+__device__ __forceinline__ uint64_t sd_value(uint64_t w) { return w & ((1ull << 40) - 1u); }
 
 // One 1024-thread block per entry block, taken by ticket in the order the blocks start (so a block
 // waiting on its predecessors waits only for blocks already running). Per entry: in the stream?, shared with the
@@ -88,7 +93,7 @@ __global__ void __launch_bounds__(kPlanBlock) plan_stream_kernel(const uint64_t*
     __shared__ uint64_t s_prefix;
     __shared__ uint32_t s_eb;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t ep = sa.epoch & 0xFFFFFu;
+    const uint32_t ep = sa.epoch & kLbEpochMask;
     if (threadIdx.x == 0) {
         // one ticket per block; the block taking the last one resets the counter for the next call
         // (a wrong start value could only misorder the blocks, never index past them)
@@ -143,10 +148,10 @@ __global__ void __launch_bounds__(kPlanBlock) plan_stream_kernel(const uint64_t*
                 bool ready = true;
                 if (p >= 0) {
                     w = __hip_atomic_load(&sa.sdesc[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ready = (uint32_t)(w >> 44) == ep && ((w >> 42) & 3u) != 0u;
+                    ready = sd_tag(w) == ep && sd_status(w) != 0u;
                 }
                 // the nearest inclusive prefix in the window (lanes in order of distance)
-                const uint64_t pmask = __ballot(p >= 0 && ready && ((w >> 42) & 3u) == 2u);
+                const uint64_t pmask = __ballot(p >= 0 && ready && sd_status(w) == 2u);
                 const int stop = pmask ? __builtin_ctzll(pmask) : 64;
                 // every word up to it must be there; otherwise wait and read the window again
                 const uint64_t rmask = __ballot(ready);
@@ -155,7 +160,7 @@ __global__ void __launch_bounds__(kPlanBlock) plan_stream_kernel(const uint64_t*
                     __builtin_amdgcn_s_sleep(1);
                     continue;
                 }
-                uint64_t part = (p >= 0 && lane <= stop) ? (w & ((1ull << 42) - 1u)) : 0u;
+                uint64_t part = (p >= 0 && lane <= stop) ? sd_value(w) : 0u;
 #pragma unroll
                 for (int d = 1; d < 64; d <<= 1) part += (uint64_t)__shfl_xor((unsigned long long)part, d);
                 prefix += part;

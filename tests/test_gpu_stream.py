@@ -189,3 +189,40 @@ def test_many_entry_blocks_lookback(gpu):
     for k in rng.integers(0, n, 2000):
         o, l = int(offs[k]), int(lens[k])
         assert got[3][k] == oracle.resume(ck.CRC32C, 0, host[o:o + l].tobytes()), k
+
+
+def test_lookback_words_after_plan_calls(gpu):
+    """The stream route's look-back words live in a region of their own (StreamScratch::lookback_words):
+    chunked-plan and stream calls of different sizes alternate on one stream with no sync between
+    them (the plan's descriptors fill the shared scratch the words once shared), and every stream
+    digest equals the plan's; the plan's equal the oracle on a sample."""
+    import torch
+    rng = np.random.default_rng(15)
+    size = 192 << 20
+    base = torch.empty(size, dtype=torch.uint8, device=gpu)
+    ck.fill_splitmix64(base, 6)
+    batches = []
+    for n, hi in ((200_000, 300), (60_000, 5000), (300_000, 120), (20_000, 2000)):
+        lens = rng.integers(1, hi, n)
+        offs = np.concatenate([[0], np.cumsum(lens[:-1])])
+        assert offs[-1] + lens[-1] <= size
+        batches.append((offs, lens, torch.from_numpy(offs.astype(np.int64)).to(gpu),
+                        torch.from_numpy(lens.astype(np.int32)).to(gpu)))
+    outs = []
+    for rep in range(3):
+        for offs, lens, d_off, d_len in batches:
+            for mode in (2, 3):
+                ck.set_plan_mode(mode)
+                outs.append((mode, len(outs) // 2 % len(batches), ck.crc_batch(ck.CRC32C, base, d_off, d_len)))
+    torch.cuda.synchronize(gpu)
+    host = base.cpu().numpy()
+    ref = {}
+    for mode, b, t in outs:
+        if mode == 2 and b not in ref:
+            ref[b] = t.cpu().numpy().view(np.uint32)
+    for mode, b, t in outs:
+        assert (t.cpu().numpy().view(np.uint32) == ref[b]).all(), (mode, b)
+    for b, (offs, lens, _, _) in enumerate(batches):
+        for k in rng.integers(0, len(offs), 300):
+            o, l = int(offs[k]), int(lens[k])
+            assert ref[b][k] == oracle.resume(ck.CRC32C, 0, host[o:o + l].tobytes()), (b, k)
