@@ -660,6 +660,39 @@ def test_plan_geometries(gpu, geom):
         ck.set_plan_geometry()
 
 
+@pytest.mark.parametrize("geom", [(8, 1, 16), (16, 8, 16), (4, 16, 16)])
+def test_plan_combine_paths_other_chunk_sizes(gpu, geom):
+    """The wave and block combines at chunk sizes other than 4 KiB (their X, X^64, X^1024 and power
+    tables are built per chunk size): entries of 65..4096 chunks and of more than 4096 chunks beside
+    short ones, seeded, both polynomials."""
+    import torch
+    lanes, steps, _ = geom
+    ch = 16 * lanes * steps
+    ck.set_plan_mode(2)
+    ck.set_plan_geometry(*geom)
+    try:
+        rng = np.random.default_rng(ch)
+        lens = rng.integers(0, 3000, 300).astype(np.int64)
+        lens[5::40] = rng.integers(65 * ch, 4096 * ch, lens[5::40].size)
+        lens[7] = 4096 * ch + 1
+        lens[150] = 4100 * ch + 333
+        lens[151] = 3 * 4096 * ch - 5
+        offs = np.concatenate([[0], np.cumsum(lens[:-1] + 13)]).astype(np.int64) + 1
+        size = int(offs[-1] + lens[-1] + 100)
+        base = torch.empty(size, dtype=torch.uint8, device=gpu)
+        ck.fill_splitmix64(base, ch)
+        host = base.cpu().numpy()
+        seeds = rng.integers(0, 2**32, lens.size, dtype=np.uint64).astype(np.uint32)
+        for algo in (ck.CRC32C, ck.CRC32):
+            got = ck.crc_batch(algo, base, torch.from_numpy(offs).to(gpu), torch.from_numpy(lens.astype(np.int32)).to(gpu),
+                               seeds=torch.from_numpy(seeds.view(np.int32)).to(gpu), sync_check=True)
+            want = oracle.batch(algo, host, offs, lens, seeds=seeds)
+            bad = np.nonzero(got.cpu().numpy().view(np.uint32) != want)[0]
+            assert len(bad) == 0, (algo, lens[bad[:10]].tolist())
+    finally:
+        ck.set_plan_geometry()
+
+
 @pytest.mark.parametrize("pinned", [False, True])
 def test_host_batch_pipelined_segments(gpu, pinned):
     """Host-memory batches spanning several 64 MiB staging segments (sorted, packed), one entry
