@@ -6,6 +6,9 @@ Usage (GPU box): python3 tools/ab_libs.py [lib.so ...]
 Default libraries: bookkeeper_amd/libbkdigest.so and every tools/variants/lib_*.so.
 Workloads: zipf (config 3), zipf crc32, zipf < 1 KiB bucket, packed 64 B, indexed 4 KiB, uniform 4 KiB.
 Each library's digests must equal the first library's, bit for bit.
+Environment: AB_WORK (workload names), AB_ROUNDS, AB_MODE (plan mode), AB_SMALL / AB_SHORT_MEAN
+(short-entry class bound and gate), AB_LANES (direct-kernel lanes), AB_PF (chunk-kernel loads in
+flight), AB_GEOM (plan geometry lanes,steps,merge), AB_NOCHECK (skip the digest comparison).
 """
 import ctypes
 import glob
