@@ -526,7 +526,7 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--zipf-align", type=int, default=1, help="diagnostic: align Zipf entries")
-    ap.add_argument("--plan-mode", type=int, default=0, help="0 auto, 1 direct, 2 chunked plan, 3 stream route")
+    ap.add_argument("--plan-mode", type=int, default=0, help="0 auto, 1 direct, 2 chunked plan")
     ap.add_argument("--no-buckets", action="store_true", help="zipf: skip the per-bucket timings")
     ap.add_argument("--pageable", action="store_true", help="host4k: pageable instead of pinned host buffer")
     ap.add_argument("--digest-op", default="both", choices=["both", "verify", "package"],

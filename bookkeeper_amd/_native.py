@@ -81,11 +81,11 @@ PROTOTYPES = {
     "bkd_host_xpow8n": (_u32, [_int, _u64]),
     "bkd_set_group_lanes": (_int, [_int]),
     "bkd_set_fold_schedule": (_int, [_int]),
-    "bkd_set_stream_range_max": (_int, [_u64]),
     "bkd_set_short_class_mean": (_int, [_u64]),
     "bkd_set_plan_mode": (_int, [_int]),
     "bkd_set_plan_geometry": (_int, [_int, _int, _int]),
     "bkd_set_plan_prefetch": (_int, [_int]),
+    "bkd_set_plan_split": (_int, [_int]),
     "bkd_set_plan_small": (_int, [_u32]),
     "bkd_set_plan_serial": (_int, [_u32]),
     "bkd_get_group_lanes": (_int, [_int, _u64]),

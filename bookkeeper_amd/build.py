@@ -8,6 +8,7 @@ from __future__ import annotations
 import os
 import shutil
 import subprocess
+import threading
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
@@ -17,7 +18,7 @@ SOURCES = [os.path.join(CSRC, "bkdigest.hip")]
 # CPU route and host worker pool (plain C++, built with the host compiler)
 HOST_SOURCES = [os.path.join(CSRC, "host_crc.cpp"), os.path.join(CSRC, "host_batch.cpp")]
 DEPS = SOURCES + HOST_SOURCES + [os.path.join(CSRC, f) for f in (
-    "crc_kernels.hpp", "crc_tables.hpp", "plan_kernels.hpp", "stream_kernels.hpp", "host_crc.hpp", "host_batch.hpp")] + [os.path.join(ROOT, "include", "bkdigest.h")]
+    "crc_kernels.hpp", "crc_tables.hpp", "plan_kernels.hpp", "host_crc.hpp", "host_batch.hpp")] + [os.path.join(ROOT, "include", "bkdigest.h")]
 ARCH = os.environ.get("BKD_OFFLOAD_ARCH", "gfx950")
 
 
@@ -48,7 +49,7 @@ def build_native(force: bool = False, extra_flags: list[str] | None = None, out:
         return out
     objs = []
     for src in HOST_SOURCES:
-        obj = os.path.join(CSRC, os.path.splitext(os.path.basename(src))[0] + f"_{os.getpid()}.o")
+        obj = os.path.join(CSRC, os.path.splitext(os.path.basename(src))[0] + f"_{os.getpid()}_{threading.get_ident()}.o")
         subprocess.run([cxx(), "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-pthread", "-c", src, "-o", obj],
                        check=True)
         objs.append(obj)

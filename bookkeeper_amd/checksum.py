@@ -384,13 +384,13 @@ def set_fold_schedule(schedule: int) -> None:
 
 
 def set_plan_mode(mode: int) -> None:
-    """0 = auto, 1 = one entry per lane group, 2 = chunked plan, 3 = stream route (indexed batches)."""
+    """0 = auto, 1 = one entry per lane group, 2 = chunked plan (indexed batches)."""
     check(lib().bkd_set_plan_mode(mode))
 
 
-def set_stream_range_max(lines: int) -> None:
-    """Stream route: lines per range above which every entry is taken whole (default 2^22)."""
-    check(lib().bkd_set_stream_range_max(lines))
+def set_plan_split(head_waves: int = -1) -> None:
+    """Chunk-kernel waves per block on the plan's heads: -1 auto (default), 0 none, 1..15 fixed."""
+    check(lib().bkd_set_plan_split(head_waves))
 
 
 def set_plan_small(max_bytes: int = 192) -> None:

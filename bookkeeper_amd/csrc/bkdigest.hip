@@ -25,7 +25,6 @@
 #include "../../include/bkdigest.h"
 #include "crc_kernels.hpp"
 #include "plan_kernels.hpp"
-#include "stream_kernels.hpp"
 #include "crc_tables.hpp"
 #include "host_batch.hpp"
 #include "host_crc.hpp"
@@ -74,52 +73,7 @@ struct StreamScratch {
     // PlanRun word of the plans enqueued on this stream and the epoch of the latest one
     uint32_t* run = nullptr;
     uint32_t* uni = nullptr;  // PlanRun uniform-lengths word (the epoch of the call it holds for)
-    uint32_t* ticket = nullptr;  // the stream route's entry-block ticket (StreamArgs::ticket), 0 between calls
     uint32_t epoch = 0;
-    // Decoupled look-back words (the stream route's positions): a region that holds nothing else, so
-    // a word not yet written by this call holds zero or an earlier call's word, never other data.
-    // Each call tags its words with the low bits of lb_calls (bkd::kLbEpochMask); the region is zeroed
-    // when allocated and whenever those bits wrap, so no earlier word can carry this call's tag.
-    uint64_t* lb = nullptr;
-    size_t lb_cap = 0;  // words
-    uint64_t lb_calls = 0;
-    hipError_t lookback_words(hipStream_t st, size_t words, uint32_t* tag, uint64_t** out) {
-        bool zero = false;
-        if (lb_cap < words) {
-            if (lb) {  // work already enqueued on this stream may still use the old region
-                const hipError_t e = hipStreamSynchronize(st);
-                if (e != hipSuccess) return e;
-                (void)hipFree(lb);
-            }
-            lb = nullptr;
-            lb_cap = 0;
-            const size_t want = words + words / 4 + 64;
-            hipError_t e = hipMalloc((void**)&lb, want * sizeof(uint64_t));
-            if (e != hipSuccess) return e;
-            lb_cap = want;
-            zero = true;
-        }
-        ++lb_calls;
-        *tag = (uint32_t)(lb_calls & bkd::kLbEpochMask);
-        if (zero || *tag == 0u) {
-            const hipError_t e = hipMemsetAsync(lb, 0, lb_cap * sizeof(uint64_t), st);
-            if (e != hipSuccess) return e;
-        }
-        *out = lb;
-        return hipSuccess;
-    }
-    hipError_t ticket_word(hipStream_t st, uint32_t** out) {
-        if (!ticket) {
-            hipError_t e = hipMalloc((void**)&ticket, sizeof(uint32_t));
-            if (e == hipSuccess) e = hipMemsetAsync(ticket, 0, sizeof(uint32_t), st);
-            if (e != hipSuccess) {
-                ticket = nullptr;
-                return e;
-            }
-        }
-        *out = ticket;
-        return hipSuccess;
-    }
     // verify gate word (verify_gate_kernel) and the epoch of the latest verify on this stream
     uint32_t* vflag = nullptr;
     uint32_t vepoch = 0;
@@ -215,7 +169,6 @@ struct DeviceState {
     int cus = 0;
     uint32_t* tables[2][kNumLaneChoices] = {};  // [algo][lane choice] compact operator images
     uint32_t* xinv[2] = {};       // [algo] x^(-8k), k = 0..127: removes the plan's zero padding
-    uint32_t* xpw[2] = {};        // [algo] x^(1024 * 2^k), k = 0..63: the stream route's powers of a line
     std::shared_mutex maps_mu;    // guards xtab and scratch
     std::map<uint64_t, uint32_t*> xtab;  // (algo, CH) -> x^(8*CH) operator for the plan's combine
     std::map<hipStream_t, std::unique_ptr<StreamScratch>> scratch;
@@ -224,8 +177,7 @@ struct DeviceState {
 std::mutex g_mu;  // device initialisation only
 DeviceState g_dev[kMaxDevices];
 std::atomic<int> g_forced_lanes{0};
-std::atomic<uint64_t> g_stream_max_tl{1ull << 22};  // bkd_set_stream_range_max (StreamArgs::maxtl)
-std::atomic<int> g_plan_mode{0};  // 0 auto, 1 direct (one entry per group), 2 chunked plan, 3 stream route
+std::atomic<int> g_plan_mode{0};  // 0 auto, 1 direct (one entry per group), 2 chunked plan
 
 // Chunked plan geometry (bkd_set_plan_geometry): lanes per group, steps per full chunk
 // (CH = 16 * lanes * jc bytes) and the head-merge threshold in bytes.
@@ -233,7 +185,10 @@ std::atomic<int> g_plan_lanes{8};
 std::atomic<int> g_plan_jc{32};
 std::atomic<int> g_plan_merge{16};
 std::atomic<int> g_fold_sched{0};  // bkd_set_fold_schedule: 0 by the measured clock, 1 fixed, 2 low-clock
-std::atomic<int> g_plan_pf{2};  // loads in flight per lane in the chunk kernel (2, 4 or 8)
+std::atomic<int> g_plan_pf{2};
+// Waves per chunk-kernel block that take the plan's heads while the others take its full chunks
+// (bkd_set_plan_split; -1: from the plan's histogram on the device, 0: every wave walks the list)
+std::atomic<int> g_plan_head_waves{-1};  // loads in flight per lane in the chunk kernel (2, 4 or 8)
 // Short-entry class of indexed batches: entries of <= this many bytes skip the plan and run in
 // their own launch (4-lane groups, next entry loaded during the current one). 0 = none.
 constexpr int kSmallLanes = 4;
@@ -321,11 +276,6 @@ int init_device_locked(int dev) {
         for (uint32_t k = 0; k < 128; ++k) inv[k] = bkd::gf2::xpow_neg8(algo, k);
         BKD_HIP(hipMalloc(&ds.xinv[algo], sizeof(inv)));
         BKD_HIP(hipMemcpy(ds.xinv[algo], inv, sizeof(inv), hipMemcpyHostToDevice));
-        uint32_t pw[64];
-        pw[0] = bkd::gf2::xpow(algo, 1024);
-        for (int k = 1; k < 64; ++k) pw[k] = bkd::gf2::mul(algo, pw[k - 1], pw[k - 1]);
-        BKD_HIP(hipMalloc(&ds.xpw[algo], sizeof(pw)));
-        BKD_HIP(hipMemcpy(ds.xpw[algo], pw, sizeof(pw), hipMemcpyHostToDevice));
     }
     BKD_HIP(hipSetDevice(prev));
     ds.ready.store(true, std::memory_order_release);
@@ -456,69 +406,17 @@ template <int G>
 void launch_plan_chunks(const bkd::PlanRun& run, const uint8_t* base, const bkd::PlanDesc* descs,
                         const uint32_t* count, const uint32_t* tab,
                         uint32_t* out, uint32_t* partials, const bkd::PlanDirectSrc& ov, int blocks, hipStream_t st,
-                        uint32_t* err, int pf) {
+                        uint32_t* err, int pf, const bkd::PlanSplit& sp) {
     // pf: read once by launch_plan (one value per call)
     if (pf == 8)
         hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 8, kNT, bkd::PlanDirectSrc>), dim3((unsigned)blocks),
-                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err);
+                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err, sp);
     else if (pf == 4)
         hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 4, kNT, bkd::PlanDirectSrc>), dim3((unsigned)blocks),
-                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err);
+                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err, sp);
     else
         hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 2, kNT, bkd::PlanDirectSrc>), dim3((unsigned)blocks),
-                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err);
-}
-
-// Indexed batch through the stream route (stream_kernels.hpp): positions (one launch, decoupled
-// look-back), the range kernel, the combine; stream-ordered, no host sync.
-int launch_stream(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, const uint64_t* offsets,
-                  const uint32_t* lengths, uint64_t n, const uint32_t* seeds, uint32_t seed_all, uint32_t* out,
-                  hipStream_t st, uint32_t mis) {
-    const uint32_t nb = (uint32_t)((n + bkd::kPlanBlock - 1) / bkd::kPlanBlock);
-    const uint32_t ngroups = (uint32_t)ds.cus * (uint32_t)(bkd::kBlock / 8);
-    Carver cv;
-    const size_t o_hdr = cv.take(64), o_pos = cv.take((size_t)n * 8),
-                 o_rec = cv.take((size_t)n * 16), o_pf = cv.take((size_t)ngroups * 4),
-                 o_pl = cv.take((size_t)ngroups * 4);
-    StreamScratch& sc = scratch_for(ds, st);
-    std::lock_guard<std::recursive_mutex> lk(sc.mu);
-    uint8_t* sb = nullptr;
-    uint32_t* err = nullptr;
-    uint32_t* ticket = nullptr;
-    uint64_t* lbw = nullptr;
-    uint32_t tag = 0;
-    hipError_t e = sc.get(0, cv.used, st, &sb);
-    if (e == hipSuccess) e = sc.flag(st, &err);
-    if (e == hipSuccess) e = sc.ticket_word(st, &ticket);
-    if (e == hipSuccess) e = sc.lookback_words(st, nb, &tag, &lbw);
-    if (e != hipSuccess) return fail(BKD_ERR_NOMEM, std::string("stream scratch: ") + hipGetErrorString(e));
-    bkd::StreamArgs sa{};
-    sa.sdesc = lbw;
-    sa.shdr = Carver::at<uint64_t>(sb, o_hdr);
-    sa.spos = Carver::at<uint64_t>(sb, o_pos);
-    sa.srec = Carver::at<bkd::u32x4>(sb, o_rec);
-    sa.pfirst = Carver::at<uint32_t>(sb, o_pf);
-    sa.plast = Carver::at<uint32_t>(sb, o_pl);
-    sa.ticket = ticket;
-    sa.ngroups = ngroups;
-    sa.mis = mis;
-    sa.epoch = tag;
-    sa.maxtl = g_stream_max_tl.load();
-    const uint32_t* tab = ds.tables[algo][lane_index(8)];
-    const uint32_t* btab = tab + bkd::gf2::byte_table_offset(8);
-    hipLaunchKernelGGL(bkd::plan_stream_kernel, dim3(nb), dim3(bkd::kPlanBlock), 0, st, offsets, lengths, seeds, seed_all,
-                       size, n, nb, sa);
-    hipLaunchKernelGGL((bkd::crc_stream_ranges_kernel<kNT>), dim3(ds.cus), dim3(bkd::kBlock), 0, st, base, size, offsets,
-                       lengths, seeds, seed_all, n, tab, out, err, sa);
-#ifndef BKD_PLAN_GRID
-#define BKD_PLAN_GRID 2
-#endif
-    const uint32_t cgrid = std::min<uint32_t>(nb, (uint32_t)BKD_PLAN_GRID * (uint32_t)ds.cus);
-    hipLaunchKernelGGL(bkd::stream_combine_kernel, dim3(cgrid), dim3(1024), 0, st, base, offsets, lengths, seeds, seed_all,
-                       size, n, nb, btab, ds.xinv[algo], bkd::gf2::poly(algo), ds.xpw[algo], sa, out, err);
-    e = hipGetLastError();
-    if (e != hipSuccess) return fail(BKD_ERR_HIP, std::string("stream kernels: ") + hipGetErrorString(e));
-    return BKD_OK;
+                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err, sp);
 }
 
 // Indexed batch through the chunked plan (plan_kernels.hpp): five stream-ordered kernels, no
@@ -532,8 +430,6 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     if (n == 0) return BKD_OK;
     if (ext_flag) short_class = direct_gate = false;
     if (n >= 0xFFFFFFF0ull) return fail(BKD_ERR_INVALID_ARG, "indexed batches hold fewer than 2^32 - 16 entries");
-    const int mode = g_plan_mode.load();
-    if (mode == 3) short_class = false;  // the stream route forced: every entry is the stream's
     const int G = g_plan_lanes.load();
     bkd::PlanGeo pg;
     pg.step = 16u * (uint32_t)G;
@@ -565,12 +461,6 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     const uint64_t capacity = std::min<uint64_t>(n + (size + 128u * n) / pg.ch + 16, 0xFFFFFFF0ull);
     const uint32_t nb = (uint32_t)((n + bkd::kPlanBlock - 1) / bkd::kPlanBlock);
     const uint32_t ncols = bkd::plan_ncols(pg);
-    // The stream route (stream_kernels.hpp, DESIGN.md §3 "Stream route"): plan mode 3, any index
-    // order, gaps or overlaps, at the default geometry (8-lane groups; the range kernel numbers
-    // device lines and entries in 32 bits). Not the automatic choice: on config 3 it measured
-    // 1.54 ms against the chunked plan's 1.16 ms (entry boundaries cost the whole wave).
-    if (BKD_STREAM && mode == 3 && G == 8 && size < (1ull << 38) && n < (1ull << 30) && !ext_flag)
-        return launch_stream(ds, algo, base, size, offsets, lengths, n, seeds, seed_all, out, st, pg.mis);
     Carver cv;
     const size_t o_blk = cv.take((size_t)nb * ncols * 4), o_live = cv.take((size_t)nb * 4),
                  o_bok = cv.take((size_t)nb * 4),
@@ -634,12 +524,21 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
                        lengths, seeds, seed_all, size, n, pg, capacity, blkoff, pslot, hslot, hdr, descs, reps, blive, nb, run);
     const uint32_t* tab = ds.tables[algo][lane_index(G)];
     const bkd::PlanDirectSrc ov{n, offsets, lengths, seeds, seed_all, size, out, pslot, hdr, capacity, false};
+#ifndef BKD_HEAD_CUS
+#define BKD_HEAD_CUS 0  // A/B builds: the heads on this many whole CUs instead of waves of every CU
+#endif
+    const int hw = g_plan_head_waves.load();
+    bkd::PlanSplit sp{hdr + bkd::kHdrBase, pg.jc, pg.nbins, 0u, hw < 0 ? bkd::kSplitAuto : (uint32_t)hw};
+    {
+        const uint32_t hb = (uint32_t)BKD_HEAD_CUS & ~7u;
+        if (hb != 0u && hb < (uint32_t)ds.cus) sp.head_blocks = hb;
+    }
     switch (G) {
-        case 4: launch_plan_chunks<4>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
-        case 8: launch_plan_chunks<8>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
-        case 16: launch_plan_chunks<16>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
-        case 32: launch_plan_chunks<32>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
-        default: launch_plan_chunks<64>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
+        case 4: launch_plan_chunks<4>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf, sp); break;
+        case 8: launch_plan_chunks<8>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf, sp); break;
+        case 16: launch_plan_chunks<16>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf, sp); break;
+        case 32: launch_plan_chunks<32>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf, sp); break;
+        default: launch_plan_chunks<64>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf, sp); break;
     }
     const uint32_t* btab = tab + bkd::gf2::byte_table_offset(G);
     hipLaunchKernelGGL(bkd::plan_combine_kernel, dim3(std::min(nb * reps, pgrid)), dim3(1024), 0, st, base, offsets, lengths, seeds,
@@ -654,7 +553,7 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
 bool indexed_direct(uint64_t size) {
     const int mode = g_plan_mode.load();
     // plan descriptors hold a biased 41-bit window start (PlanDesc): buffers >= 1 TiB take the direct kernel
-    return mode == 1 || (mode == 0 && size <= kDirectMaxBytes) || size >= bkd::kPlanMaxSize;  // (3: stream)
+    return mode == 1 || (mode == 0 && size <= kDirectMaxBytes) || size >= bkd::kPlanMaxSize;
 }
 
 // route: -1 decided here from the plan mode and the buffer size, else the caller's decision
@@ -1325,12 +1224,6 @@ int bkd_init(int device) {
 
 const char* bkd_last_error(void) { return t_err.c_str(); }
 
-int bkd_set_stream_range_max(uint64_t lines) {
-    if (lines < 4u) return fail(BKD_ERR_INVALID_ARG, "stream range bound must be at least 4 lines");
-    g_stream_max_tl.store(lines);
-    return BKD_OK;
-}
-
 int bkd_set_fold_schedule(int schedule) {
     if (schedule < 0 || schedule > 2) return fail(BKD_ERR_INVALID_ARG, "fold schedule must be 0, 1 or 2");
     g_fold_sched.store(schedule);
@@ -1344,9 +1237,15 @@ int bkd_set_group_lanes(int lanes) {
 }
 
 int bkd_set_plan_mode(int mode) {
-    if (mode < 0 || mode > 3)
-        return fail(BKD_ERR_INVALID_ARG, "plan mode must be 0 (auto), 1 (direct), 2 (plan) or 3 (stream)");
+    if (mode < 0 || mode > 2)
+        return fail(BKD_ERR_INVALID_ARG, "plan mode must be 0 (auto), 1 (direct) or 2 (plan)");
     g_plan_mode.store(mode);
+    return BKD_OK;
+}
+
+int bkd_set_plan_split(int head_waves) {
+    if (head_waves < -1 || head_waves > 15) return fail(BKD_ERR_INVALID_ARG, "head waves must be -1 (auto) or 0..15");
+    g_plan_head_waves.store(head_waves);
     return BKD_OK;
 }
 
@@ -1488,9 +1387,8 @@ int bkd_stream_release(void* stream) {
         BKD_HIP(hipStreamSynchronize(st));  // the stream's own work is done with them
         for (int k = 0; k < 3; ++k)
             if (sc->buf[k]) BKD_HIP(hipFree(sc->buf[k]));
-        for (uint32_t* w : {sc->err, sc->run, sc->uni, sc->vflag, sc->ticket})
+        for (uint32_t* w : {sc->err, sc->run, sc->uni, sc->vflag})
             if (w) BKD_HIP(hipFree(w));
-        if (sc->lb) BKD_HIP(hipFree(sc->lb));
         if (sc->h_err) BKD_HIP(hipHostFree(sc->h_err));
     }
     return status;

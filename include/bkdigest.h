@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define BKD_ABI_VERSION 5
+#define BKD_ABI_VERSION 6
 
 /* only the entry points below are exported (the library is built with -fvisibility=hidden) */
 #ifndef BKD_API
@@ -276,9 +276,8 @@ BKD_API uint32_t bkd_host_xpow8n(int algo, uint64_t nbytes);
 BKD_API int bkd_set_group_lanes(int lanes);
 /* Indexed-batch strategy: 0 = automatic (one entry per lane group when the base buffer is <= 256 KiB,
  * else the chunked plan with the short-entry class when the buffer holds at most 1 KiB per entry),
- * 1 = one entry per lane group, 2 = always the chunked plan, 3 = the stream route (the
- * entries' lines end to end, one range of lines per lane group, any index order; no short-entry
- * class). Verify pipelines keep the chunked plan. */
+ * 1 = one entry per lane group, 2 = always the chunked plan. Any other value (the removed stream
+ * route was mode 3) returns BKD_ERR_INVALID_ARG. */
 BKD_API int bkd_set_plan_mode(int mode);
 /* Chunked-plan geometry: lanes per group (4, 8, 16, 32 or 64), steps per full chunk (chunk = 16 * lanes *
  * steps bytes, <= 32 KiB) and the head-merge threshold in bytes (a head chunk shorter than this
@@ -296,6 +295,11 @@ BKD_API int bkd_set_short_class_mean(uint64_t max_bytes_per_entry);
 /* Entries of the plan shorter than `bytes` (16..64, default 16) skip the chunk kernel: the
  * combine kernel computes each with one thread (slice-by-16 over its 16-byte windows). */
 BKD_API int bkd_set_plan_serial(uint32_t bytes);
+/* How the plan's chunk kernel divides its waves: -1 (default) = chosen on the device from the plan's
+ * step-count histogram (the heads' share of the work, DESIGN.md §3 "Wave split"), 0 = every wave walks
+ * the whole list (full chunks first, then heads), 1..15 = that many of each block's 16 waves take the
+ * heads while the others take the full chunks. Digests are identical either way. */
+BKD_API int bkd_set_plan_split(int head_waves);
 /* Register double-buffer depth of the plan's chunk kernel (2, 4 or 8 loads per lane). */
 BKD_API int bkd_set_plan_prefetch(int loads_in_flight);
 /* Fold schedule of the one-entry-per-group kernels (uniform, direct indexed, package payloads):
@@ -303,10 +307,6 @@ BKD_API int bkd_set_plan_prefetch(int loads_in_flight);
  * 2 GHz), 1 = always the compiler's schedule, 2 = always the low-clock schedule
  * (16 table lookups in flight per step). Results are identical; only the speed differs. */
 BKD_API int bkd_set_fold_schedule(int schedule);
-/* Stream route: lines per range above which the range kernel takes every entry whole, one per lane
- * group (only a batch of heavily overlapping huge entries reaches the default 2^22; tests lower it to
- * exercise that path). >= 4. */
-BKD_API int bkd_set_stream_range_max(uint64_t lines);
 BKD_API int bkd_get_group_lanes(int algo, uint64_t mean_len);
 
 #ifdef __cplusplus

@@ -100,7 +100,7 @@ def test_golden_vectors(gpu):
         assert (got == want).all(), lanes
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+@pytest.mark.parametrize("mode", [0, 1, 2])
 def test_golden_batch_4096(gpu, mode):
     """SURVEY.md §8c's 4096-entry reference-generated set (lengths 0..70000, unaligned offsets into
     a 32 MiB stream, seeded) through the automatic route, the direct kernel and the chunk plan."""
@@ -247,11 +247,11 @@ def test_uniform_tiny_entries_auto_one_lane(gpu):
 
 
 @pytest.mark.parametrize("algo", [ck.CRC32C, ck.CRC32])
-@pytest.mark.parametrize("lanes,mode", [(l, 1) for l in LANES] + [(0, 2), (0, 0), (0, 3)])
+@pytest.mark.parametrize("lanes,mode", [(l, 1) for l in LANES] + [(0, 2), (0, 0)])
 def test_indexed_ragged_unaligned(gpu, algo, lanes, mode):
     """Random lengths 0..70000, random (unaligned, overlapping) offsets, random per-entry seeds;
-    mode 1 = one entry per lane group, mode 2 = chunked plan, mode 0 = automatic, 3 = stream route
-    (every entry a jump here: one tile run each)."""
+    mode 1 = one entry per lane group, mode 2 = chunked plan, mode 0 = automatic (the direct kernel
+    here: a 3 MB base buffer)."""
     import torch
     ck.set_group_lanes(lanes)
     ck.set_plan_mode(mode)
@@ -781,12 +781,40 @@ def test_zipf_full_size_every_entry_vs_reference(gpu):
     try:
         for algo in (ck.CRC32C, ck.CRC32):
             want, _ = _threaded_reference(algo, host, offs, lens)
-            for mode in (0, 2, 1, 3):  # auto (the bench's route: stream), chunked plan, direct, stream
+            for mode in (0, 2, 1):  # auto (the bench's route: the chunked plan), chunked plan forced, direct
                 ck.set_plan_mode(mode)
                 got = ck.crc_batch(algo, base, d_off, d_len, sync_check=True).cpu().numpy().view(np.uint32)
                 bad = np.nonzero(got != want)[0]
                 assert bad.size == 0, (algo, mode, bad.size, bad[:5].tolist(), lens[bad[:5]].tolist())
     finally:
+        ck.set_plan_mode(0)
+
+
+@pytest.mark.parametrize("head_waves", [-1, 0, 1, 4, 8, 15])
+def test_plan_wave_split_bit_exact(gpu, head_waves):
+    """The chunk kernel's wave split (bkd_set_plan_split: the last head_waves waves of every block
+    take the heads while the others take the full chunks; -1 = from the plan's histogram) changes
+    only the schedule: 256 K Zipf entries through the plan equal the reference's digests for every
+    split, both polynomials, with per-entry seeds."""
+    import torch
+    from bench import zipf_index
+    offs, lens = zipf_index(1 << 18)
+    total = int(offs[-1] + lens[-1])
+    base = torch.empty(total, dtype=torch.uint8, device=gpu)
+    ck.fill_splitmix64(base, 17)
+    d_off = torch.from_numpy(offs).to(gpu)
+    d_len = torch.from_numpy(lens.astype(np.int32)).to(gpu)
+    host = base.cpu().numpy()
+    ck.set_plan_mode(2)
+    ck.set_plan_split(head_waves)
+    try:
+        for algo in (ck.CRC32C, ck.CRC32):
+            want, _ = _threaded_reference(algo, host, offs, lens)
+            got = ck.crc_batch(algo, base, d_off, d_len, sync_check=True).cpu().numpy().view(np.uint32)
+            bad = np.nonzero(got != want)[0]
+            assert bad.size == 0, (algo, head_waves, bad.size, bad[:5].tolist())
+    finally:
+        ck.set_plan_split(-1)
         ck.set_plan_mode(0)
 
 

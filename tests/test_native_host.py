@@ -28,7 +28,20 @@ def test_library_exports_every_declared_symbol():
     assert set(declared) <= exported
     # nothing but the declared entry points leaks as a C symbol (C++ kernel stubs are mangled)
     assert {x for x in exported if not x.startswith("_Z") and not x.startswith("__hip")} == set(declared)
-    assert L.bkd_abi_version() == 5  # 3: bkd_stream_release; 4: host batch routes, bkd_host_release; 5: bkd_set_fold_schedule
+    # 3: bkd_stream_release; 4: host batch routes, bkd_host_release; 5: bkd_set_fold_schedule;
+    # 6: the stream route and bkd_set_stream_range_max removed
+    assert L.bkd_abi_version() == 6
+
+
+def test_plan_mode_three_is_gone():
+    """The stream route (plan mode 3) was removed from the library: the setter
+    rejects it and leaves the mode it had."""
+    L = _native.lib()
+    assert L.bkd_set_plan_mode(3) == -1  # BKD_ERR_INVALID_ARG
+    assert not hasattr(L, "bkd_set_stream_range_max")
+    for mode in (0, 1, 2):
+        assert L.bkd_set_plan_mode(mode) == 0
+    assert L.bkd_set_plan_mode(0) == 0
 
 
 def test_library_contains_gfx950_code():

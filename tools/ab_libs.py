@@ -41,7 +41,7 @@ def main(paths):
             L.bkd_set_plan_small(int(os.environ["AB_SMALL"]))
         if os.environ.get("AB_SHORT_MEAN") and hasattr(L, "bkd_set_short_class_mean"):
             L.bkd_set_short_class_mean(int(os.environ["AB_SHORT_MEAN"]))
-        if os.environ.get("AB_MODE") and hasattr(L, "bkd_set_plan_mode"):  # 0 auto, 1 direct, 2 plan, 3 stream
+        if os.environ.get("AB_MODE") and hasattr(L, "bkd_set_plan_mode"):  # 0 auto, 1 direct, 2 plan
             L.bkd_set_plan_mode(int(os.environ["AB_MODE"]))
         if os.environ.get("AB_LANES"):  # lanes per group of the one-entry-per-group kernels
             assert L.bkd_set_group_lanes(int(os.environ["AB_LANES"])) == 0

@@ -47,11 +47,6 @@ for step in "$@"; do
        run pmc_write_$cfg 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write_$cfg -o pmc -- python3 $R/bench.py $extra --steps 5 --warmup 1) || exit 1
       if [ $cfg = zipf ]; then zipf_bytes; python3 tools/pmc_summary.py $O/pmc_fetch_zipf $O/pmc_write_zipf zipf $ZB bkd::crc_plan_chunks_kernel > $O/pmc_z.json || exit 1
       else python3 tools/pmc_summary.py $O/pmc_fetch_uniform $O/pmc_write_uniform uniform4k $((1048576*4100)) > $O/pmc_u.json || exit 1; fi ;;
-    pmc_zipf_stream)  # the stream route (plan mode 3): FETCH/WRITE passes, main kernel = the range kernel
-      (cd /tmp && export TMPDIR=/tmp &&
-       run pmc_fetch_zs 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_zs -o pmc -- python3 $R/bench.py --config zipf --plan-mode 3 --no-buckets --no-cpu-baseline --steps 5 --warmup 1 &&
-       run pmc_write_zs 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write_zs -o pmc -- python3 $R/bench.py --config zipf --plan-mode 3 --no-buckets --no-cpu-baseline --steps 5 --warmup 1) || exit 1
-      zipf_bytes; python3 tools/pmc_summary.py $O/pmc_fetch_zs $O/pmc_write_zs zipf_stream $ZB "bkd::crc_stream_ranges_kernel" > $O/pmc_zs.json || exit 1 ;;
     ab:*) run ab_$(date +%s%N) 900 python3 tools/ab_libs.py $(echo ${step#ab:} | tr , " ") ;;
     kstats:*) lib=${step#kstats:}; nm=$(basename $lib .so); (cd /tmp && export TMPDIR=/tmp && AB_ROUNDS=${AB_ROUNDS:-2} run kstats_$nm 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kstats_$nm -o k -- python3 $R/tools/ab_libs.py $R/$lib) || exit 1
       python3 tools/kstats.py $O/kstats_$nm > $O/kstats_$nm.txt && cat $O/kstats_$nm.txt ;;
