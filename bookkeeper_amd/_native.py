@@ -85,7 +85,6 @@ PROTOTYPES = {
     "bkd_set_plan_mode": (_int, [_int]),
     "bkd_set_plan_geometry": (_int, [_int, _int, _int]),
     "bkd_set_plan_prefetch": (_int, [_int]),
-    "bkd_set_plan_split": (_int, [_int]),
     "bkd_set_plan_small": (_int, [_u32]),
     "bkd_set_plan_serial": (_int, [_u32]),
     "bkd_get_group_lanes": (_int, [_int, _u64]),

@@ -388,11 +388,6 @@ def set_plan_mode(mode: int) -> None:
     check(lib().bkd_set_plan_mode(mode))
 
 
-def set_plan_split(head_waves: int = -1) -> None:
-    """Chunk-kernel waves per block on the plan's heads: -1 auto (default), 0 none, 1..15 fixed."""
-    check(lib().bkd_set_plan_split(head_waves))
-
-
 def set_plan_small(max_bytes: int = 192) -> None:
     """Entries of <= max_bytes (<= 512) of a planned indexed batch run in the short-entry launch (0 = none)."""
     check(lib().bkd_set_plan_small(max_bytes))

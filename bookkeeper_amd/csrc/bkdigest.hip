@@ -185,10 +185,7 @@ std::atomic<int> g_plan_lanes{8};
 std::atomic<int> g_plan_jc{32};
 std::atomic<int> g_plan_merge{16};
 std::atomic<int> g_fold_sched{0};  // bkd_set_fold_schedule: 0 by the measured clock, 1 fixed, 2 low-clock
-std::atomic<int> g_plan_pf{2};
-// Waves per chunk-kernel block that take the plan's heads while the others take its full chunks
-// (bkd_set_plan_split; -1: from the plan's histogram on the device, 0: every wave walks the list)
-std::atomic<int> g_plan_head_waves{-1};  // loads in flight per lane in the chunk kernel (2, 4 or 8)
+std::atomic<int> g_plan_pf{2};  // loads in flight per lane in the chunk kernel (2, 4 or 8)
 // Short-entry class of indexed batches: entries of <= this many bytes skip the plan and run in
 // their own launch (4-lane groups, next entry loaded during the current one). 0 = none.
 constexpr int kSmallLanes = 4;
@@ -406,17 +403,17 @@ template <int G>
 void launch_plan_chunks(const bkd::PlanRun& run, const uint8_t* base, const bkd::PlanDesc* descs,
                         const uint32_t* count, const uint32_t* tab,
                         uint32_t* out, uint32_t* partials, const bkd::PlanDirectSrc& ov, int blocks, hipStream_t st,
-                        uint32_t* err, int pf, const bkd::PlanSplit& sp) {
+                        uint32_t* err, int pf) {
     // pf: read once by launch_plan (one value per call)
     if (pf == 8)
         hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 8, kNT, bkd::PlanDirectSrc>), dim3((unsigned)blocks),
-                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err, sp);
+                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err);
     else if (pf == 4)
         hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 4, kNT, bkd::PlanDirectSrc>), dim3((unsigned)blocks),
-                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err, sp);
+                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err);
     else
         hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 2, kNT, bkd::PlanDirectSrc>), dim3((unsigned)blocks),
-                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err, sp);
+                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err);
 }
 
 // Indexed batch through the chunked plan (plan_kernels.hpp): five stream-ordered kernels, no
@@ -514,7 +511,8 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
 #define BKD_PLAN_GRID 2
 #endif
     const uint32_t pgrid = BKD_PLAN_GRID ? (uint32_t)BKD_PLAN_GRID * (uint32_t)ds.cus : 0xFFFFFFFFu;
-    hipLaunchKernelGGL(bkd::plan_count_kernel, dim3(std::min(nb, pgrid)), dim3(bkd::kPlanBlock), 0, st, offsets,
+    const uint32_t cgrid = std::min((nb + bkd::kCountBlocks - 1u) / bkd::kCountBlocks, pgrid);
+    hipLaunchKernelGGL(bkd::plan_count_kernel, dim3(cgrid), dim3(bkd::kPlanBlock), 0, st, offsets,
                        lengths, size, n, pg, blk, blive, nb, run, bok);
     hipLaunchKernelGGL(bkd::plan_scan_kernel, dim3(ncols + (gate ? 1u : 0u)), dim3(bkd::kPlanBlock), 0, st, blk, nb,
                        blkoff, hdr, run, ncols, bok);
@@ -524,21 +522,12 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
                        lengths, seeds, seed_all, size, n, pg, capacity, blkoff, pslot, hslot, hdr, descs, reps, blive, nb, run);
     const uint32_t* tab = ds.tables[algo][lane_index(G)];
     const bkd::PlanDirectSrc ov{n, offsets, lengths, seeds, seed_all, size, out, pslot, hdr, capacity, false};
-#ifndef BKD_HEAD_CUS
-#define BKD_HEAD_CUS 0  // A/B builds: the heads on this many whole CUs instead of waves of every CU
-#endif
-    const int hw = g_plan_head_waves.load();
-    bkd::PlanSplit sp{hdr + bkd::kHdrBase, pg.jc, pg.nbins, 0u, hw < 0 ? bkd::kSplitAuto : (uint32_t)hw};
-    {
-        const uint32_t hb = (uint32_t)BKD_HEAD_CUS & ~7u;
-        if (hb != 0u && hb < (uint32_t)ds.cus) sp.head_blocks = hb;
-    }
     switch (G) {
-        case 4: launch_plan_chunks<4>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf, sp); break;
-        case 8: launch_plan_chunks<8>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf, sp); break;
-        case 16: launch_plan_chunks<16>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf, sp); break;
-        case 32: launch_plan_chunks<32>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf, sp); break;
-        default: launch_plan_chunks<64>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf, sp); break;
+        case 4: launch_plan_chunks<4>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
+        case 8: launch_plan_chunks<8>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
+        case 16: launch_plan_chunks<16>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
+        case 32: launch_plan_chunks<32>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
+        default: launch_plan_chunks<64>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
     }
     const uint32_t* btab = tab + bkd::gf2::byte_table_offset(G);
     hipLaunchKernelGGL(bkd::plan_combine_kernel, dim3(std::min(nb * reps, pgrid)), dim3(1024), 0, st, base, offsets, lengths, seeds,
@@ -1240,12 +1229,6 @@ int bkd_set_plan_mode(int mode) {
     if (mode < 0 || mode > 2)
         return fail(BKD_ERR_INVALID_ARG, "plan mode must be 0 (auto), 1 (direct) or 2 (plan)");
     g_plan_mode.store(mode);
-    return BKD_OK;
-}
-
-int bkd_set_plan_split(int head_waves) {
-    if (head_waves < -1 || head_waves > 15) return fail(BKD_ERR_INVALID_ARG, "head waves must be -1 (auto) or 0..15");
-    g_plan_head_waves.store(head_waves);
     return BKD_OK;
 }
 

@@ -1336,24 +1336,6 @@ __device__ __forceinline__ void plan_chunks_loop(const uint32_t* lds, uint32_t l
 // chunk's first loads are issued during the previous chunk (chunk_fold), X/Y register sets
 // alternating.
 // After its chunks, the grid computes the entries the plan could not hold (`ov`, normally empty).
-// How the chunk kernel's grid splits the list (DESIGN.md §3 "CU split"): the last `head_blocks`
-// blocks take the heads (list positions from the first bin below `jc`, i.e. after every bin of
-// >= jc steps), the other blocks the full chunks — concurrently, on disjoint CUs: the full chunks
-// are bound by HBM, the heads by their per-chunk instruction chain. head_blocks == 0: every block
-// walks the whole list. `cols`: the plan's column totals (hdr[kHdrBase ..]).
-struct PlanSplit {
-    const uint32_t* cols;
-    uint32_t jc;
-    uint32_t nbins;
-    uint32_t head_blocks;
-    uint32_t head_waves;  // instead of blocks: the last head_waves waves of every block take the heads
-};
-// head_waves = kSplitAuto: chosen in the kernel from the plan's histogram, the heads' share of the
-// work with each head chunk weighted as kSplitChunkSteps steps more than it has (its finish, seed
-// and pad handling — calibrated on config 3, where 4 of 16 waves measured best).
-constexpr uint32_t kSplitAuto = 0xFFFFFFFFu;
-constexpr uint32_t kSplitChunkSteps = 6u;
-
 template <int G, int PF, bool NT, class OvSrc>
 __global__ void __launch_bounds__(kBlock) crc_plan_chunks_kernel(const uint8_t* __restrict__ base,
                                                                  const PlanDesc* __restrict__ descs,
@@ -1361,8 +1343,7 @@ __global__ void __launch_bounds__(kBlock) crc_plan_chunks_kernel(const uint8_t* 
                                                                  const uint32_t* __restrict__ tables,
                                                                  uint32_t* __restrict__ out,
                                                                  uint32_t* __restrict__ partials, OvSrc ov,
-                                                                 PlanRun run, uint32_t* __restrict__ err,
-                                                                 PlanSplit split) {
+                                                                 PlanRun run, uint32_t* __restrict__ err) {
     using Gm = Geo<G>;
     if (!run.plan_entries()) return;  // only short entries
     __shared__ __attribute__((aligned(16))) uint32_t lds[Gm::kLdsWords];
@@ -1380,61 +1361,7 @@ __global__ void __launch_bounds__(kBlock) crc_plan_chunks_kernel(const uint8_t* 
     const uint64_t gid = (uint64_t)blockIdx.x * (kBlock / G) + (uint64_t)(threadIdx.x / G);
     // count[1]: the list position of the first chunk of at most PF + 1 steps (plan_emit_kernel)
     const uint64_t nmain = n ? std::min<uint64_t>(n, count[1]) : 0u;
-    // this block's part of the list [lo, hi) (short tail from hmain) and its place among the blocks
-    // that share that part
-    uint64_t lo = 0u, hi = n, hmain = nmain;
-    constexpr uint32_t kWaves = kBlock / 64;
-    const uint32_t wave = threadIdx.x >> 6;
-    uint32_t ru = blockIdx.x * kWaves + wave, nu = gridDim.x * kWaves;  // this wave's rank among its role's
-    const bool by_blocks = split.head_blocks != 0u && split.head_blocks < gridDim.x;
-    if ((by_blocks || split.head_waves != 0u) && n != 0u) {  // kernel-uniform
-        uint64_t P = 0u, wf = 0u, wh = 0u;  // chunks of >= jc steps (the list's first part); work in steps
-        for (uint32_t j = 0; j < split.nbins; ++j) {
-            const uint64_t c = split.cols[j];
-            if (j >= split.jc) {
-                P += c;
-                wf += c * j;
-            } else {
-                wh += c * (j + kSplitChunkSteps);
-            }
-        }
-        if (split.head_waves == kSplitAuto) {
-            // the heads' share of the work, in whole waves of 16; a share under 2 or over 12 waves
-            // leaves one part too small to be worth a role of its own (every wave walks the list)
-            const uint64_t hw = (wh * kWaves * 2u + (wh + wf)) / (2u * (wh + wf) + 1u);
-            split.head_waves = (hw >= 2u && hw <= 12u) ? (uint32_t)hw : 0u;
-        }
-        const bool by_waves = split.head_waves != 0u && split.head_waves < kWaves;
-        if ((by_blocks || by_waves) && P > 0u && P < n && P <= nmain) {
-            if (by_blocks) {
-                const uint32_t b1 = gridDim.x - split.head_blocks;
-                if (blockIdx.x >= b1) {
-                    ru = (blockIdx.x - b1) * kWaves + wave;
-                    nu = split.head_blocks * kWaves;
-                    lo = P;
-                } else {
-                    nu = b1 * kWaves;
-                    hi = hmain = P;
-                }
-            } else {
-                const uint32_t w1 = kWaves - split.head_waves;
-                if (wave >= w1) {
-                    ru = blockIdx.x * split.head_waves + (wave - w1);
-                    nu = gridDim.x * split.head_waves;
-                    lo = P;
-                } else {
-                    ru = blockIdx.x * w1 + wave;
-                    nu = gridDim.x * w1;
-                    hi = hmain = P;
-                }
-            }
-        }
-    }
-    const uint64_t pgroups = (uint64_t)nu * (64 / G);
-    const uint64_t pgid = (uint64_t)ru * (64 / G) + (uint64_t)((threadIdx.x & 63) / G);
-    if (pgid < hi - lo)
-        plan_chunks_loop<G, PF, NT>(lds, lanereg, g, base, descs + lo, hi - lo, hmain - lo, pgid, pgroups, out,
-                                    partials);
+    if (gid < n) plan_chunks_loop<G, PF, NT>(lds, lanereg, g, base, descs, n, nmain, gid, ngroups, out, partials);
     if (nov) groups_loop<G, PF, NT>(lds, lanereg, g, base, ov, nov, gid, ngroups, err);
 }
 

@@ -168,60 +168,81 @@ __host__ __device__ __forceinline__ uint32_t plan_ncols(const PlanGeo& pg) { ret
 // Per-block column counts (plan_scan_kernel turns them into per-block offsets and totals).
 // blive[b]: entries of block b that the plan itself handles (not the short-entry class); emit and
 // combine skip blocks without any (a batch of short entries costs them one word per block).
+// Entry blocks per plan_count block: thread t counts entry t of each of kCountBlocks consecutive
+// entry blocks, their index words requested together (the kernel is bound by load latency: one
+// entry per thread ran config 3's 1 M entries in two rounds of 13 us, four per thread in one of 7).
+constexpr uint32_t kCountBlocks = 4;
+
 __global__ void __launch_bounds__(kPlanBlock) plan_count_kernel(const uint64_t* __restrict__ offsets,
                                                                 const uint32_t* __restrict__ lengths, uint64_t size,
                                                                 uint64_t n, PlanGeo pg, uint32_t* __restrict__ blk,
                                                                 uint32_t* __restrict__ blive, uint32_t nb, PlanRun run,
                                                                 uint32_t* __restrict__ bok) {
     if (!run.plan_entries()) return;
-    __shared__ uint32_t col[kMaxJC + 2];
-    __shared__ uint32_t live, bad;
+    __shared__ uint32_t col[kCountBlocks][kMaxJC + 2];
+    __shared__ uint32_t live[kCountBlocks], bad[kCountBlocks];
     const uint32_t ncols = plan_ncols(pg);
     const uint32_t ref = bok ? lengths[0] : 0u;  // the uniformity ballot's reference length
-    for (uint32_t eb = blockIdx.x; eb < nb; eb += gridDim.x) {  // entry blocks of 1024, grid stride
-    for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) col[k] = 0u;
-    if (threadIdx.x == 0) {
-        live = 0u;
-        bad = 0u;
+    const uint32_t ngb = (nb + kCountBlocks - 1u) / kCountBlocks;
+    for (uint32_t gb = blockIdx.x; gb < ngb; gb += gridDim.x) {  // kCountBlocks entry blocks at a time, grid stride
+    for (uint32_t k = threadIdx.x; k < kCountBlocks * (kMaxJC + 2); k += kPlanBlock) (&col[0][0])[k] = 0u;
+    if (threadIdx.x < kCountBlocks) {
+        live[threadIdx.x] = 0u;
+        bad[threadIdx.x] = 0u;
     }
     __syncthreads();
-    const uint64_t i = (uint64_t)eb * kPlanBlock + threadIdx.x;
-    uint32_t full = 0u, mine = 0u;
-    bool ok = true;  // length within the band of the reference (PlanRun::in_band)
-    if (i < n) {
-        const uint32_t l = lengths[i];
-        // without a short class every offset is needed: loaded beside its length (one round trip);
-        // with one, only for the plan's own entries (a batch of short entries reads no offsets)
-        const uint64_t o0 = pg.small == 0u ? offsets[i] : 0u;
-        ok = PlanRun::in_band(l, ref);
-        if (!is_small(l, pg)) {
-            mine = 1u;
-            const EntryPlan p = plan_entry(pg.small == 0u ? o0 : offsets[i], l, size, pg);
-            if (p.kind == 0) {
-                if (p.jh != pg.jc) atomicAdd(&col[p.jh], 1u);
-                full = p.full;
+    // the lengths (and, without a short class, offsets) of the thread's entries requested at once;
+    // with a short class offsets are loaded only for the plan's own entries
+    uint32_t l[kCountBlocks];
+    uint64_t o[kCountBlocks];
+#pragma unroll
+    for (uint32_t k = 0; k < kCountBlocks; ++k) {
+        const uint64_t i = (uint64_t)(gb * kCountBlocks + k) * kPlanBlock + threadIdx.x;
+        const uint64_t ic = i < n ? i : n - 1u;
+        l[k] = lengths[ic];
+        o[k] = pg.small == 0u ? offsets[ic] : 0u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kCountBlocks; ++k) {
+        const uint64_t i = (uint64_t)(gb * kCountBlocks + k) * kPlanBlock + threadIdx.x;
+        uint32_t full = 0u, mine = 0u;
+        bool ok = true;  // length within the band of the reference (PlanRun::in_band)
+        if (i < n) {
+            ok = PlanRun::in_band(l[k], ref);
+            if (!is_small(l[k], pg)) {
+                mine = 1u;
+                const EntryPlan p = plan_entry(pg.small == 0u ? o[k] : offsets[i], l[k], size, pg);
+                if (p.kind == 0) {
+                    if (p.jh != pg.jc) atomicAdd(&col[k][p.jh], 1u);
+                    full = p.full;
+                }
             }
         }
-    }
-    // every entry adds to these columns: one LDS atomic per wave instead of 64
+        // every entry adds to these columns: one LDS atomic per wave instead of 64
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        full += (uint32_t)__shfl_xor((int)full, d);
-        mine += (uint32_t)__shfl_xor((int)mine, d);
-    }
-    const bool wave_ok = __all(ok);
-    if ((threadIdx.x & 63) == 0) {
-        if (full) atomicAdd(&col[pg.jc], full);
-        if (mine) atomicAdd(&live, mine);
-        if (!wave_ok) bad = 1u;  // (a per-wave min/max with global atomics cost +330 us per 1 M entries)
+        for (int d = 1; d < 64; d <<= 1) {
+            full += (uint32_t)__shfl_xor((int)full, d);
+            mine += (uint32_t)__shfl_xor((int)mine, d);
+        }
+        const bool wave_ok = __all(ok);
+        if ((threadIdx.x & 63) == 0) {
+            if (full) atomicAdd(&col[k][pg.jc], full);
+            if (mine) atomicAdd(&live[k], mine);
+            if (!wave_ok) bad[k] = 1u;  // (a per-wave min/max with global atomics cost +330 us per 1 M entries)
+        }
     }
     __syncthreads();
-    for (uint32_t k = threadIdx.x; k < ncols; k += kPlanBlock) blk[(uint64_t)k * nb + eb] = col[k];
-    if (threadIdx.x == 0) {
-        blive[eb] = live;
-        if (bok) bok[eb] = bad ^ 1u;
+#pragma unroll
+    for (uint32_t k = 0; k < kCountBlocks; ++k) {
+        const uint32_t eb = gb * kCountBlocks + k;
+        if (eb >= nb) break;  // block-uniform
+        for (uint32_t c = threadIdx.x; c < ncols; c += kPlanBlock) blk[(uint64_t)c * nb + eb] = col[k][c];
+        if (threadIdx.x == 0) {
+            blive[eb] = live[k];
+            if (bok) bok[eb] = bad[k] ^ 1u;
+        }
     }
-    __syncthreads();  // col/live are reset for the next entry block
+    __syncthreads();  // col/live are reset for the next entry blocks
     }
 }
 

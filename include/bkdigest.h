@@ -295,11 +295,6 @@ BKD_API int bkd_set_short_class_mean(uint64_t max_bytes_per_entry);
 /* Entries of the plan shorter than `bytes` (16..64, default 16) skip the chunk kernel: the
  * combine kernel computes each with one thread (slice-by-16 over its 16-byte windows). */
 BKD_API int bkd_set_plan_serial(uint32_t bytes);
-/* How the plan's chunk kernel divides its waves: -1 (default) = chosen on the device from the plan's
- * step-count histogram (the heads' share of the work, DESIGN.md §3 "Wave split"), 0 = every wave walks
- * the whole list (full chunks first, then heads), 1..15 = that many of each block's 16 waves take the
- * heads while the others take the full chunks. Digests are identical either way. */
-BKD_API int bkd_set_plan_split(int head_waves);
 /* Register double-buffer depth of the plan's chunk kernel (2, 4 or 8 loads per lane). */
 BKD_API int bkd_set_plan_prefetch(int loads_in_flight);
 /* Fold schedule of the one-entry-per-group kernels (uniform, direct indexed, package payloads):

@@ -790,34 +790,6 @@ def test_zipf_full_size_every_entry_vs_reference(gpu):
         ck.set_plan_mode(0)
 
 
-@pytest.mark.parametrize("head_waves", [-1, 0, 1, 4, 8, 15])
-def test_plan_wave_split_bit_exact(gpu, head_waves):
-    """The chunk kernel's wave split (bkd_set_plan_split: the last head_waves waves of every block
-    take the heads while the others take the full chunks; -1 = from the plan's histogram) changes
-    only the schedule: 256 K Zipf entries through the plan equal the reference's digests for every
-    split, both polynomials, with per-entry seeds."""
-    import torch
-    from bench import zipf_index
-    offs, lens = zipf_index(1 << 18)
-    total = int(offs[-1] + lens[-1])
-    base = torch.empty(total, dtype=torch.uint8, device=gpu)
-    ck.fill_splitmix64(base, 17)
-    d_off = torch.from_numpy(offs).to(gpu)
-    d_len = torch.from_numpy(lens.astype(np.int32)).to(gpu)
-    host = base.cpu().numpy()
-    ck.set_plan_mode(2)
-    ck.set_plan_split(head_waves)
-    try:
-        for algo in (ck.CRC32C, ck.CRC32):
-            want, _ = _threaded_reference(algo, host, offs, lens)
-            got = ck.crc_batch(algo, base, d_off, d_len, sync_check=True).cpu().numpy().view(np.uint32)
-            bad = np.nonzero(got != want)[0]
-            assert bad.size == 0, (algo, head_waves, bad.size, bad[:5].tolist())
-    finally:
-        ck.set_plan_split(-1)
-        ck.set_plan_mode(0)
-
-
 def test_concurrent_callers(gpu):
     """§8b threading: one shared library instance called from several host threads at once, each
     with its own HIP stream (device batches through the plan, the direct kernel and the uniform

@@ -167,7 +167,10 @@ def main(paths):
             if ref is None:
                 ref = out[:cnt].clone()
             if not os.environ.get("AB_NOCHECK"):  # (measurement-only variants compute wrong digests)
-                assert torch.equal(out[:cnt], ref), f"{name}: digests differ between libraries"
+                if not torch.equal(out[:cnt], ref):
+                    bad = torch.nonzero(out[:cnt] != ref).flatten()
+                    raise AssertionError(f"{name}: {L._name} differs from the first library on {bad.numel()} "
+                                         f"entries, first {bad[:5].tolist()}")
         for _ in range(ROUNDS):
             for lname, L in libs.items():
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
