@@ -1,6 +1,8 @@
 /*
  * Java side of the batch surface of libbkdigest (include/bkdigest.h), bound by the JNI shim
- * native/jni/bkdigest_jni.c. Not compiled in this repository's image (no JDK); the native
+ * native/jni/bkdigest_jni.c. It lives in circe-checksum beside the IntHash providers (that module
+ * already depends on native-library-common for Sse42Crc32C's loader; bookkeeper-server depends on
+ * circe-checksum, never the other way). Not compiled in this repository's image (no JDK); the native
  * declarations below are the table tests/test_jni_signatures.py checks the shim's exports against,
  * and tests/test_jni_shim.py executes every one of those natives through a fake JNIEnv.
  *
@@ -8,9 +10,9 @@
  * (bookkeeper-server/.../client/BatchedReadOp.java:164-190) and PendingAddOp packages one entry per
  * add (PendingAddOp.java:261, DigestManager.java:117-181). These entry points take whole batches.
  */
-package org.apache.bookkeeper.proto.checksum;
+package com.scurrilous.circe.checksum;
 
-import com.scurrilous.circe.utils.NativeUtils;
+import org.apache.bookkeeper.common.util.nativelib.NativeUtils;
 
 public final class GpuDigest {
     /** Algorithm ids of the C-ABI (BKD_CRC32C / BKD_CRC32). */
@@ -31,8 +33,9 @@ public final class GpuDigest {
         boolean loaded = false;
         boolean device = false;
         try {
-            // the same jar location and loader as the circe natives (Sse42Crc32C.java:33-40,
-            // NativeUtils.java:54-99): the shim is packaged as the circe library
+            // the same jar location and loader as the circe natives (Sse42Crc32C.java:18-19,33-40;
+            // native-library-common NativeUtils.java:54-116): the shim is packaged as the circe
+            // library, so this is the one library Sse42Crc32C loads too
             NativeUtils.loadLibraryFromJar("/lib/libcirce-checksum." + NativeUtils.libType());
             loaded = true;
             device = deviceCount() > 0 && init(0) == 0;

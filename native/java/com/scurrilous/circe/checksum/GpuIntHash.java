@@ -1,6 +1,7 @@
 /*
  * IntHash over libbkdigest (GpuDigest's natives), first in Crc32cIntChecksum's provider chain when
- * the library loads (INTEGRATION.md §1). Not compiled in this repository's image (no JDK).
+ * the library loads and a device initialises (GpuProviderChain, INTEGRATION.md §1). Not compiled in
+ * this repository's image (no JDK).
  *
  * Interface: circe-checksum/.../checksum/IntHash.java:23-35. Buffer dispatch follows the other
  * providers (JniIntHash.java:45-53): a native address when the ByteBuf has one, the backing array
@@ -10,7 +11,6 @@
 package com.scurrilous.circe.checksum;
 
 import io.netty.buffer.ByteBuf;
-import org.apache.bookkeeper.proto.checksum.GpuDigest;
 
 public class GpuIntHash implements IntHash {
 

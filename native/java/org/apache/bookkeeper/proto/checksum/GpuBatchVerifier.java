@@ -1,0 +1,84 @@
+/*
+ * The batched verify hook for BatchedReadOp (bookkeeper-server/.../client/BatchedReadOp.java:164-190).
+ * The reference verifies the entries of a batched read one by one and keeps the verified prefix:
+ *
+ *     for (int i = 0; i < bufList.size(); i++) {
+ *         try { lh.macManager.verifyDigestAndReturnData(eId + i, buffer); verifiedEntries++; }
+ *         catch (BKException.BKDigestMatchException e) { ...; break; }
+ *     }
+ *
+ * With this class that loop becomes one call,
+ *
+ *     int verifiedEntries = GpuBatchVerifier.verifiedPrefix(lh.macManager, eId, bufList);
+ *
+ * followed by the reference's own handling of verifiedEntries (re-read from another replica when it
+ * is 0, the read-op digest-mismatch counter when it is below bufList.size()). The whole ByteBufList
+ * goes to libbkdigest's bkd_digest_verify_batch_host (header CRC, payload CRC, digest compare, ledger
+ * and entry id checks — DigestManager.java:226-283 — per entry, the verified prefix returned). CRC32C
+ * and CRC32 digest managers with direct (memory-address) buffers take that path; anything else (MAC or
+ * dummy digests, heap or composite buffers, no library, a library error) runs the reference's loop
+ * unchanged. It lives in DigestManager's package for the manager's ledgerId. Not compiled in this
+ * repository's image (no JDK): tests/test_java_sources.py resolves its imports against the reference.
+ */
+package org.apache.bookkeeper.proto.checksum;
+
+import com.scurrilous.circe.checksum.GpuDigest;
+import io.netty.buffer.ByteBuf;
+import io.netty.buffer.PooledByteBufAllocator;
+import org.apache.bookkeeper.client.BKException;
+import org.apache.bookkeeper.util.ByteBufList;
+
+public final class GpuBatchVerifier {
+
+    private GpuBatchVerifier() {
+    }
+
+    /** How many leading entries of bufList (entry ids firstEntryId, firstEntryId + 1, ...) verify. */
+    public static int verifiedPrefix(DigestManager dm, long firstEntryId, ByteBufList bufList) {
+        final int n = bufList.size();
+        final int algo = dm instanceof CRC32CDigestManager ? GpuDigest.CRC32C
+                : dm instanceof CRC32DigestManager ? GpuDigest.CRC32 : -1;
+        boolean direct = n > 0 && algo >= 0 && GpuDigest.isLoaded();
+        for (int i = 0; direct && i < n; i++) {
+            direct = bufList.getBuffer(i).hasMemoryAddress();
+        }
+        if (!direct) {
+            return serialPrefix(dm, firstEntryId, bufList);
+        }
+        // frame addresses (u64), lengths (u32) and per-entry status (i32), little-endian direct buffers
+        final ByteBuf addrs = PooledByteBufAllocator.DEFAULT.directBuffer(8 * n);
+        final ByteBuf lens = PooledByteBufAllocator.DEFAULT.directBuffer(4 * n);
+        final ByteBuf status = PooledByteBufAllocator.DEFAULT.directBuffer(4 * n);
+        try {
+            if (!addrs.hasMemoryAddress() || !lens.hasMemoryAddress() || !status.hasMemoryAddress()) {
+                return serialPrefix(dm, firstEntryId, bufList);
+            }
+            for (int i = 0; i < n; i++) {
+                final ByteBuf b = bufList.getBuffer(i);
+                addrs.writeLongLE(b.memoryAddress() + b.readerIndex());
+                lens.writeIntLE(b.readableBytes());
+            }
+            final long rc = GpuDigest.verifyBatch(algo, dm.ledgerId, firstEntryId, false, addrs.memoryAddress(),
+                    lens.memoryAddress(), n, status.memoryAddress());
+            return rc < 0 ? serialPrefix(dm, firstEntryId, bufList) : (int) rc;
+        } finally {
+            addrs.release();
+            lens.release();
+            status.release();
+        }
+    }
+
+    // BatchedReadOp.java:175-189 without its logging and retry: the verified prefix
+    private static int serialPrefix(DigestManager dm, long firstEntryId, ByteBufList bufList) {
+        int verified = 0;
+        for (int i = 0; i < bufList.size(); i++) {
+            try {
+                dm.verifyDigestAndReturnData(firstEntryId + i, bufList.getBuffer(i));
+                verified++;
+            } catch (BKException.BKDigestMatchException e) {
+                break;
+            }
+        }
+        return verified;
+    }
+}

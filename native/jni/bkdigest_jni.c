@@ -12,7 +12,7 @@
  *                                  address returns 0 (:39-40); the config handle is ignored
  *                                  (results never depend on the chunk ladder)
  *      allocConfig / freeConfig -> bkd_circe_alloc_config / bkd_circe_free_config (same validation)
- * 2. org.apache.bookkeeper.proto.checksum.GpuDigest — the batch surface the reference lacks
+ * 2. com.scurrilous.circe.checksum.GpuDigest — the batch surface the reference lacks
  *    (INTEGRATION.md §2): device count/init, per-call resume for CRC32C and CRC32, host-memory
  *    batches, and the host-resident DigestManager verify/package batches.
  *
@@ -116,15 +116,15 @@ JNIEXPORT void JNICALL Java_com_scurrilous_circe_crc_Sse42Crc32C_freeConfig(JNIE
     bkd_circe_free_config((int64_t)config);
 }
 
-/* ---- org.apache.bookkeeper.proto.checksum.GpuDigest (new batch surface) ---------------------- */
+/* ---- com.scurrilous.circe.checksum.GpuDigest (new batch surface) ----------------------------- */
 
-JNIEXPORT jint JNICALL Java_org_apache_bookkeeper_proto_checksum_GpuDigest_deviceCount(JNIEnv* env, jclass cls) {
+JNIEXPORT jint JNICALL Java_com_scurrilous_circe_checksum_GpuDigest_deviceCount(JNIEnv* env, jclass cls) {
     (void)env;
     (void)cls;
     return bkd_device_count();
 }
 
-JNIEXPORT jint JNICALL Java_org_apache_bookkeeper_proto_checksum_GpuDigest_init(JNIEnv* env, jclass cls, jint dev) {
+JNIEXPORT jint JNICALL Java_com_scurrilous_circe_checksum_GpuDigest_init(JNIEnv* env, jclass cls, jint dev) {
     (void)env;
     (void)cls;
     return bkd_init(dev);
@@ -132,7 +132,7 @@ JNIEXPORT jint JNICALL Java_org_apache_bookkeeper_proto_checksum_GpuDigest_init(
 
 /* resume(algo, current, address, length): a host address (Netty memoryAddress()); CRC32 included, for
  * CRC32DigestManager's DirectMemoryCRC32Digest (CRC32DigestManager.java:28-87) */
-JNIEXPORT jint JNICALL Java_org_apache_bookkeeper_proto_checksum_GpuDigest_resumeAddress(JNIEnv* env, jclass cls,
+JNIEXPORT jint JNICALL Java_com_scurrilous_circe_checksum_GpuDigest_resumeAddress(JNIEnv* env, jclass cls,
                                                                                        jint algo, jint current,
                                                                                        jlong address, jlong len) {
     (void)env;
@@ -147,7 +147,7 @@ JNIEXPORT jint JNICALL Java_org_apache_bookkeeper_proto_checksum_GpuDigest_resum
 
 /* resumeArray(algo, current, byte[], offset, len): a heap buffer (ByteBuf.array()); the Java side has
  * checked the bounds (AbstractIncrementalIntHash.java:62-69) */
-JNIEXPORT jint JNICALL Java_org_apache_bookkeeper_proto_checksum_GpuDigest_resumeArray(JNIEnv* env, jclass cls,
+JNIEXPORT jint JNICALL Java_com_scurrilous_circe_checksum_GpuDigest_resumeArray(JNIEnv* env, jclass cls,
                                                                                      jint algo, jint current,
                                                                                      jbyteArray input, jint offset,
                                                                                      jint len) {
@@ -156,7 +156,7 @@ JNIEXPORT jint JNICALL Java_org_apache_bookkeeper_proto_checksum_GpuDigest_resum
 }
 
 /* batch over one host region: offsets/lengths/seeds/out are addresses of direct buffers */
-JNIEXPORT jint JNICALL Java_org_apache_bookkeeper_proto_checksum_GpuDigest_resumeBatch(
+JNIEXPORT jint JNICALL Java_com_scurrilous_circe_checksum_GpuDigest_resumeBatch(
     JNIEnv* env, jclass cls, jint algo, jlong base, jlong size, jlong offs, jlong lens, jlong n, jlong seeds,
     jint seedAll, jlong out) {
     (void)env;
@@ -168,7 +168,7 @@ JNIEXPORT jint JNICALL Java_org_apache_bookkeeper_proto_checksum_GpuDigest_resum
 
 /* BatchedReadOp.complete over a ByteBufList (BatchedReadOp.java:164-190): frame addresses and lengths
  * in direct buffers; returns the verified prefix length (n if all verified) or a negative BKD_ERR_* */
-JNIEXPORT jlong JNICALL Java_org_apache_bookkeeper_proto_checksum_GpuDigest_verifyBatch(
+JNIEXPORT jlong JNICALL Java_com_scurrilous_circe_checksum_GpuDigest_verifyBatch(
     JNIEnv* env, jclass cls, jint algo, jlong ledgerId, jlong firstEntryId, jboolean skipEntryIdCheck,
     jlong frameAddrs, jlong frameLens, jlong n, jlong statusOut) {
     (void)env;
@@ -182,7 +182,7 @@ JNIEXPORT jlong JNICALL Java_org_apache_bookkeeper_proto_checksum_GpuDigest_veri
 }
 
 /* PendingAddOp / LedgerFragmentReplicator packaging (DigestManager.java:117-181) of n host payloads */
-JNIEXPORT jint JNICALL Java_org_apache_bookkeeper_proto_checksum_GpuDigest_packageBatch(
+JNIEXPORT jint JNICALL Java_com_scurrilous_circe_checksum_GpuDigest_packageBatch(
     JNIEnv* env, jclass cls, jint algo, jlong ledgerId, jlong entryIds, jlong lacs, jlong lengthFields,
     jlong payloadAddrs, jlong payloadLens, jlong n, jlong framesOut, jlong frameStride, jlong digestsOut) {
     (void)env;
@@ -195,7 +195,7 @@ JNIEXPORT jint JNICALL Java_org_apache_bookkeeper_proto_checksum_GpuDigest_packa
                                          (uint32_t*)(intptr_t)digestsOut);
 }
 
-JNIEXPORT jstring JNICALL Java_org_apache_bookkeeper_proto_checksum_GpuDigest_lastError(JNIEnv* env, jclass cls) {
+JNIEXPORT jstring JNICALL Java_com_scurrilous_circe_checksum_GpuDigest_lastError(JNIEnv* env, jclass cls) {
     (void)cls;
     return (*env)->NewStringUTF(env, bkd_last_error());
 }

@@ -34,7 +34,7 @@ SHIM = os.path.join(ROOT, "native", "jni", "bkdigest_jni.c")
 FAKE = os.path.join(ROOT, "tests", "jni_fake")
 CRC32C, CRC32 = 0, 1
 SSE = "Java_com_scurrilous_circe_crc_Sse42Crc32C_"
-GPU = "Java_org_apache_bookkeeper_proto_checksum_GpuDigest_"
+GPU = "Java_com_scurrilous_circe_checksum_GpuDigest_"
 
 
 def _jint(v: int) -> int:

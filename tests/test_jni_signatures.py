@@ -27,7 +27,7 @@ SSE42 = [
     ("long", "allocConfig", ["int[]"]),
     ("void", "freeConfig", ["long"]),
 ]
-# INTEGRATION.md §2, org.apache.bookkeeper.proto.checksum.GpuDigest
+# INTEGRATION.md §2, com.scurrilous.circe.checksum.GpuDigest
 GPU_DIGEST = [
     ("int", "deviceCount", []),
     ("int", "init", ["int"]),
@@ -38,7 +38,7 @@ GPU_DIGEST = [
     ("int", "packageBatch", ["int", "long", "long", "long", "long", "long", "long", "long", "long", "long", "long"]),
     ("String", "lastError", []),
 ]
-CLASSES = {"com.scurrilous.circe.crc.Sse42Crc32C": SSE42, "org.apache.bookkeeper.proto.checksum.GpuDigest": GPU_DIGEST}
+CLASSES = {"com.scurrilous.circe.crc.Sse42Crc32C": SSE42, "com.scurrilous.circe.checksum.GpuDigest": GPU_DIGEST}
 
 
 def _exports():
@@ -85,7 +85,7 @@ def test_sse42_natives_match_reference_declarations(name):
 def test_gpu_digest_java_declarations_match_table():
     """native/java/.../GpuDigest.java (the committed Java side of the batch class) declares exactly the
     natives of the table, with the same types, so the shim, the table and the Java source agree."""
-    src = os.path.join(ROOT, "native", "java", "org", "apache", "bookkeeper", "proto", "checksum", "GpuDigest.java")
+    src = os.path.join(ROOT, "native", "java", "com", "scurrilous", "circe", "checksum", "GpuDigest.java")
     text = re.sub(r"/\*.*?\*/", "", open(src).read(), flags=re.S)
     found = {}
     for m in re.finditer(r"public static native (\S+) (\w+)\(([^)]*)\);", text, flags=re.S):
