@@ -5,7 +5,7 @@ Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 la
 torch.distributed.run, one rank per GPU (``--gpus N`` without that environment starts the N ranks
 itself, through torch.distributed.run, before anything touches a GPU). A step = one launch of the
 digest engine over the whole per-GPU batch (BASELINE.json configs[1]: 1,048,576 x 4 KiB entries,
-CRC32C, seed 0, bytes = little-endian splitmix64 stream seed 42, generated on the device). Entries
+CRC32C, CRC init 0, bytes = little-endian splitmix64 stream seed 42, generated on the device). Entries
 shard across ranks with no data-path collective (weak scaling); the only collectives are the
 timing barriers, the max-over-ranks reduction and the gather of per-rank timings.
 
@@ -574,6 +574,13 @@ def run_rank(args, ck, torch, dist, world: int, rank: int, dev) -> None:
     algo = ck.CRC32C if args.algo == "crc32c" else ck.CRC32
     ck.set_group_lanes(args.lanes)
     ck.set_plan_mode(args.plan_mode)
+    # a multi-GPU line must come from N distinct GPUs: under RCCL every rank checks the gathered PCI
+    # addresses before any work, so a misconfigured job stops at once, on every rank
+    idents = gather_identity(dev, world)
+    if world > 1 and args.dist_backend == "nccl":
+        pcis = [d["pci"] for d in idents]
+        if len(set(pcis)) != len(pcis):
+            raise SystemExit(f"ranks share a GPU under nccl: {pcis}")
 
     stream = torch.cuda.current_stream(dev)
     if args.config == "host4k":
@@ -598,10 +605,11 @@ def run_rank(args, ck, torch, dist, world: int, rank: int, dev) -> None:
         if args.config == "shard8m":
             workload = {"workload": f"config 4: 64M x 4 KiB over 8 GPUs, 8M per GPU (this run: {world} GPU"
                                     f"{'s' if world > 1 else ''} x {n} entries = {n * world} x 4 KiB, weak scaling), "
-                                    f"device-resident, {args.algo}, seed 0",
+                                    f"device-resident, {args.algo}, CRC init 0, data seed 42",
                         "entries_per_gpu": n, "entry_bytes": entry_len}
         else:
-            workload = {"workload": f"{n} x {entry_len} B ledger entries per GPU, device-resident, {args.algo}, seed 0",
+            workload = {"workload": f"{n} x {entry_len} B ledger entries per GPU, device-resident, {args.algo}, "
+                                    f"CRC init 0, data seed 42",
                         "entries_per_gpu": n, "entry_bytes": entry_len}
     else:
         n = args.entries or (1 << 20)
@@ -665,13 +673,16 @@ def run_rank(args, ck, torch, dist, world: int, rank: int, dev) -> None:
 
     coll_dev = dev if args.dist_backend == "nccl" else None
     elapsed_max = max_over_ranks(elapsed, coll_dev)
-    per_rank = gather_over_ranks([elapsed, avg_kernel_s, solo_kernel_s or avg_kernel_s], coll_dev)
-    idents = gather_identity(dev, world)
-    if world > 1 and args.dist_backend == "nccl" and rank == 0:
-        # a SCALE line must come from N distinct GPUs: one PCI address per rank under RCCL
-        pcis = [d["pci"] for d in idents]
-        if len(set(pcis)) != len(pcis):
-            raise SystemExit(f"ranks share a GPU under nccl: {pcis}")
+    # N > 1: every rank checks a sample of its own shard against the C oracle after the timed region
+    # (N = 1 checks the whole batch against the reference in the cpu_baseline leg below)
+    shard_check = None
+    if world > 1 and not args.no_check:
+        shard_check = shard_parity(ck, torch, algo, args.config, base, out, n,
+                                   entry_len if args.config in ("uniform4k", "shard8m") else 0,
+                                   None if args.config in ("uniform4k", "shard8m") else (offs, lens))
+    per_rank = gather_over_ranks([elapsed, avg_kernel_s, solo_kernel_s or avg_kernel_s,
+                                  shard_check["entries"] if shard_check else 0,
+                                  float(shard_check["match"]) if shard_check else 1.0], coll_dev)
 
     total_payload = payload_bytes * world * args.steps  # every rank processes its batch once per step
     value = total_payload / elapsed_max / GIB
@@ -700,13 +711,22 @@ def run_rank(args, ck, torch, dist, world: int, rank: int, dev) -> None:
         # per GPU: its own wall rate over the timed region, its kernel time, and (N > 1) its rate when
         # it ran alone on the node in this same run; efficiency = (aggregate / N) / mean solo rate
         "per_gpu": [{"rank": r, "GiB_s": round(payload_bytes * args.steps / e / GIB, 2),
-                     "kernel_ms": round(k * 1e3, 4), "solo_GiB_s": round(payload_bytes / so / GIB, 2), **idents[r]}
-                    for r, (e, k, so) in enumerate(per_rank)],
+                     "kernel_ms": round(k * 1e3, 4), "solo_GiB_s": round(payload_bytes / so / GIB, 2), **idents[r],
+                     **({"parity_check": {"entries": int(pe), "match": bool(pm)}} if shard_check else {})}
+                    for r, (e, k, so, pe, pm) in enumerate(per_rank)],
         "per_gpu_GiB_s": round(value / world, 2),
     }
     if world > 1:
-        solo_mean = float(np.mean([payload_bytes / so / GIB for _, _, so in per_rank]))
+        solo_mean = float(np.mean([payload_bytes / so / GIB for _, _, so, _, _ in per_rank]))
         result["efficiency_vs_solo"] = round(value / world / solo_mean, 4)
+    if shard_check:
+        ok = all(bool(pm) for *_, pm in per_rank)
+        result["parity_check"] = {"entries": int(sum(pe for *_, pe, _ in per_rank)), "match": ok,
+                                  "sample": f"{SHARD_SAMPLE} entries of each rank's shard vs the C oracle"}
+        if not ok:
+            if rank == 0:
+                print(json.dumps(result), flush=True)
+            raise SystemExit("PARITY FAILURE: a rank's GPU digests differ from the oracle's")
     if args.config == "zipf" and world == 1 and not args.no_buckets:
         result["buckets"] = bucket_rates(ck, torch, algo, base, offs, lens, stream, max(3, args.steps))
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "zipf":
@@ -734,13 +754,49 @@ def run_rank(args, ck, torch, dist, world: int, rank: int, dev) -> None:
         print(json.dumps(result), flush=True)
 
 
+SHARD_SAMPLE = 65536
+
+
+def shard_parity(ck, torch, algo, config, base, out, n, entry_len, index) -> dict:
+    """Checker leg for N > 1: SHARD_SAMPLE entries of this rank's shard (evenly spaced for uniform
+    entries, the first ones of a Zipf index) against the C oracle (oracle/, test infrastructure; the
+    GPU result under test is `out` as the timed steps left it)."""
+    import oracle
+    m = min(n, SHARD_SAMPLE)
+    got_all = out.cpu().numpy().view(np.uint32)
+    if entry_len:
+        idx = np.linspace(0, n - 1, m).astype(np.int64)
+        rows = base.view(n, entry_len)[torch.from_numpy(idx).to(base.device)].cpu().numpy().reshape(-1)
+        want = oracle.uniform(algo, rows, entry_len, entry_len, m)
+        got = got_all[idx]
+    else:
+        offs, lens = index
+        span = int(offs[m - 1] + lens[m - 1])
+        host = np.ascontiguousarray(base[:span].cpu().numpy())
+        want = oracle.batch(algo, host, offs[:m], lens[:m])
+        got = got_all[:m]
+    return {"entries": m, "match": bool((got == want).all())}
+
+
+def _lib_sha256() -> str:
+    import hashlib
+    from bookkeeper_amd.build import LIB
+    with open(LIB, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
 def _pmc_traffic(config: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), or None."""
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/pmc_<config>.json), or
+    None — also None when the summary was collected on another build of libbkdigest.so than the one
+    being timed (its lib_sha256 stamp, written by tools/pmc_summary.py, must match)."""
     path = os.path.join(HERE, "profiles", f"pmc_{config}.json")
     if not os.path.exists(path):
         return None
     try:
-        return json.load(open(path)).get("hbm_bytes_per_launch")
+        pmc = json.load(open(path))
+        if pmc.get("lib_sha256") != _lib_sha256():
+            return None
+        return pmc.get("hbm_bytes_per_launch")
     except Exception:
         return None
 

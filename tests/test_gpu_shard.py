@@ -158,6 +158,11 @@ def test_bench_two_ranks_default_is_config4_shard(gpu):
         assert p["world_size_seen"] == 2 and p["device"] and p["uuid"] is not None
         assert len(p["pci"].split(":")) == 3
     assert [p["rank"] for p in res["per_gpu"]] == [0, 1]
+    # each rank checked a 65 536-entry sample of its own shard against the C
+    # oracle after the timed region, and the line carries each result
+    for p in res["per_gpu"]:
+        assert p["parity_check"] == {"entries": 65536, "match": True}
+    assert res["parity_check"]["match"] is True and res["parity_check"]["entries"] == 2 * 65536
     # whole-job value = both ranks' payload over the slowest rank's time
     total = 2 * 8388608 * 4096 * res["steps"] / (1 << 30)
     assert abs(res["value"] - total / (res["ms_per_step"] * res["steps"] / 1e3)) / res["value"] < 0.01

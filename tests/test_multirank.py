@@ -68,3 +68,27 @@ def test_single_process_reduction_is_identity():
     from bench import max_over_ranks, shard_first_word
     assert max_over_ranks(1.5) == 1.5
     assert shard_first_word(3, 1 << 20, 4096) == 3 * (1 << 20) * 512
+
+
+def test_bench_shard_parity_checker_cpu():
+    """bench.py's N > 1 checker leg (shard_parity) on CPU tensors: a rank's correct digests match
+    the oracle on the sampled entries (uniform and Zipf layouts), and one wrong sampled digest fails."""
+    import torch
+
+    import bench
+    import oracle
+    from bookkeeper_amd import checksum as ck
+    n, L = 300, 256
+    data = oracle.fill_splitmix64(n * L, 42)
+    base = torch.from_numpy(data.copy())
+    good = oracle.uniform(oracle.CRC32C, data, L, L, n)
+    out = torch.from_numpy(good.view(np.int32).copy())
+    assert bench.shard_parity(ck, torch, ck.CRC32C, "shard8m", base, out, n, L, None) == {"entries": n, "match": True}
+    out[-1] ^= 1  # the sample always includes the last entry
+    assert bench.shard_parity(ck, torch, ck.CRC32C, "shard8m", base, out, n, L, None)["match"] is False
+    offs, lens = bench.zipf_index(200)
+    zdata = oracle.fill_splitmix64(int(offs[-1] + lens[-1]), 7)
+    zgood = oracle.batch(oracle.CRC32, zdata, offs, lens)
+    zout = torch.from_numpy(zgood.view(np.int32).copy())
+    chk = bench.shard_parity(ck, torch, ck.CRC32, "zipf", torch.from_numpy(zdata.copy()), zout, 200, 0, (offs, lens))
+    assert chk == {"entries": 200, "match": True}

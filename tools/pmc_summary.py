@@ -7,12 +7,17 @@ coalesced streaming read, so read bytes = 2 * FETCH_SIZE * 1024 for the streamin
 index/descriptor kernels (plan_*) are reported separately, raw (no correction: their accesses are
 not wide streaming reads).
 
+Each summary carries lib_sha256, the sha256 of the bookkeeper_amd/libbkdigest.so the counters were
+collected on.
+
 usage: pmc_summary.py FETCH_DIR WRITE_DIR CONFIG ALGO_BYTES_PER_LAUNCH [MAIN_KERNEL [OTHER_KERNELS]]
 OTHER_KERNELS: comma-separated short names of the other kernels of the measured call (default: every
 other bkd:: kernel in the trace), e.g. the verify pipeline's gate/header/plan/finish launches when the
 same process also ran package calls."""
-import csv, glob, json, os, sys
+import csv, glob, hashlib, json, os, sys, time
 from collections import defaultdict
+
+LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bookkeeper_amd", "libbkdigest.so")
 
 
 def load(pattern):
@@ -62,7 +67,11 @@ def main(fetch_dir, write_dir, config, algo_bytes, main_kernel="bkd::crc_groups_
            "algorithmic_bytes_per_launch": algo_bytes,
            "traffic_over_algorithmic": (read_b + write_b + aux_b) / algo_bytes,
            "correction": "main kernel: read = 2 x FETCH_SIZE x 1024 (gfx950 half-count of wide streaming reads), "
-                         "write = WRITE_SIZE x 1024; other kernels raw"}
+                         "write = WRITE_SIZE x 1024; other kernels raw",
+           # provenance: the build these counters came from (bench.py attaches `traffic` only when the
+           # library it times has this hash)
+           "lib_sha256": hashlib.sha256(open(LIB, "rb").read()).hexdigest(),
+           "collected_utc": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())}
     os.makedirs("profiles", exist_ok=True)
     json.dump(out, open(f"profiles/pmc_{config}.json", "w"), indent=1)
     print(json.dumps(out))
