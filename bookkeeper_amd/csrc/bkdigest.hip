@@ -450,7 +450,9 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     // costs more than it saves where they are a minority of a large-entry batch (config 3's Zipf:
     // +54 us launch, -43 us chunk kernel). So it runs when the mean entry is at most 1 KiB.
     const uint64_t mean_max = g_short_mean_max.load();
-    pg.small = (short_class && (mean_max == UINT64_MAX || size <= mean_max * n)) ? g_plan_small.load() : 0u;
+    // size <= mean_max * n, without forming the product (it could overflow for large bounds)
+    const bool short_gate = mean_max == UINT64_MAX || size / n < mean_max || (size / n == mean_max && size % n == 0u);
+    pg.small = (short_class && short_gate) ? g_plan_small.load() : 0u;
     const uint32_t* xtab = nullptr;
     int rc = xtab_for(ds, algo, pg.ch, &xtab);
     if (rc) return rc;
@@ -498,7 +500,7 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
             const unsigned sblocks = (unsigned)std::min<uint64_t>((n + per_block - 1) / per_block, (uint64_t)ds.cus);
             hipLaunchKernelGGL((bkd::crc_groups_kernel<kSmallLanes, 2, kNT, bkd::SmallIndexedSrc>), dim3(sblocks),
                                dim3(bkd::kBlock), 0, st, base, ss, ds.tables[algo][lane_index(kSmallLanes)], err, 1);
-        } else {  // entries up to 1 KiB: 16-lane groups, an entry's four steps in one register set
+        } else {  // bounds above 192 B: kSmallLanesWide-lane groups (8: up to 512 B), an entry's PF + 1 steps in one register set
             const uint64_t per_block = bkd::kBlock / kSmallLanesWide;
             const unsigned sblocks = (unsigned)std::min<uint64_t>((n + per_block - 1) / per_block, (uint64_t)ds.cus);
             hipLaunchKernelGGL((bkd::crc_groups_kernel<kSmallLanesWide, 3, kNT, bkd::SmallIndexedSrc>), dim3(sblocks),

@@ -93,6 +93,9 @@ def main(paths):
         "packed64": (0, *idx(np.arange(n) * 64, np.full(n, 64)), n * 64),
         "packed64_64m": (0, *idx(np.arange(64 * n) * 64, np.full(64 * n, 64)), 64 * n * 64),
         "indexed4k": (0, *idx(np.arange(n) * 4096, np.full(n, 4096)), n * 4096),
+        # 1M aligned 4 KiB entries through the chunk kernel (one 2 KiB entry keeps them out of the
+        # near-uniform gate's band): the chunk loop against the uniform kernel on the same bytes
+        "plan4k": (0, *idx(np.arange(n) * 4096, np.where(np.arange(n) == 5, 2048, 4096)), n * 4096 - 2048),
         # 16 entries of 256 MiB: the stream route's inner loop with almost no entry boundary
         "big16": (0, *idx(np.arange(16) * (n * 256), np.full(16, n * 256)), 16 * n * 256),
         # 4096 entries of 1 MiB plus 7 bytes (unaligned ends), packed
