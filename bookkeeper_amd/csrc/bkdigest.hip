@@ -887,9 +887,25 @@ int host_batch_pipelined(DeviceState& ds, HostStage& hs, int algo, const uint8_t
 // ---- DigestManager batch framing: the device sequences shared by the device- and host-resident
 // entry points -------------------------------------------------------------------------------
 
+// Package, fused route (4..64-lane groups, frames apart from the payload; BKD_PACKAGE_FUSED): each lane group
+// builds its entry's header from the index arrays and folds header + payload in one pass, storing the
+// digest (crc_package_fused_kernel); package_frame_kernel then writes every frame's header and digest.
+template <int G>
+void launch_package_fused(DeviceState& ds, hipStream_t st, int algo, int64_t ledger_id, const int64_t* d_entry_ids,
+                          const int64_t* d_lacs, const int64_t* d_length_fields, const uint8_t* payload,
+                          uint64_t payload_size, const uint64_t* d_offsets, const uint32_t* d_lengths, uint64_t n,
+                          uint32_t* d_digests, uint32_t* err) {
+    const uint64_t per_block = bkd::kBlock / G;
+    const unsigned blocks = (unsigned)std::min<uint64_t>((n + per_block - 1) / per_block, (uint64_t)ds.cus);
+    hipLaunchKernelGGL((bkd::crc_package_fused_kernel<G, kPF, kNT>), dim3(blocks), dim3(bkd::kBlock), 0, st, payload,
+                       payload_size, d_offsets, d_lengths, n, ledger_id, d_entry_ids, d_lacs, d_length_fields,
+                       ds.tables[algo][lane_index(G)], d_digests, err, g_fold_sched.load());
+}
+
 // Package: header kernel (32 B BE header, header CRC as the payload's seed) -> payload CRCs through
 // the direct kernel -> digest kernel (BE digest after the header; BKD_PACKAGE_DIGEST_PASS=0 has the
-// payload groups store it instead). Out-of-range payload entries raise the stream's bounds flag.
+// payload groups store it instead) — or the fused route above, which folds the header inside the
+// payload kernel. Out-of-range payload entries raise the stream's bounds flag.
 int package_framed(DeviceState& ds, hipStream_t st, int algo, int64_t ledger_id, const int64_t* d_entry_ids,
                    const int64_t* d_lacs, const int64_t* d_length_fields, const void* d_payload,
                    uint64_t payload_size, const uint64_t* d_offsets, const uint32_t* d_lengths, uint64_t n,
@@ -905,6 +921,30 @@ int package_framed(DeviceState& ds, hipStream_t st, int algo, int64_t ledger_id,
         if (e != hipSuccess) return fail(BKD_ERR_NOMEM, std::string("bounds flag: ") + hipGetErrorString(e));
     }
     const unsigned blocks = (unsigned)((n + 255) / 256);
+#ifndef BKD_PACKAGE_FUSED
+#define BKD_PACKAGE_FUSED 1
+#endif
+    // The fused route when the frames are their own buffer (DigestManager's ByteBufList(header, data),
+    // bench.py --config verify4k: 0.674 -> 0.659 ms per 1M 4 KiB entries); frames written in place in
+    // front of their payloads keep the header-first route (0.821 vs 0.832 ms fused, profiles/r06r_*).
+    const uint64_t fr0 = (uint64_t)(uintptr_t)d_frames, fr1 = fr0 + (n - 1u) * frame_stride + 32u + mac;
+    const uint64_t pl0 = (uint64_t)(uintptr_t)d_payload, pl1 = pl0 + payload_size;
+    const bool frames_apart = fr1 <= pl0 || pl1 <= fr0;
+    if (BKD_PACKAGE_FUSED && lanes >= 4 && frames_apart) {
+        const uint8_t* pl = (const uint8_t*)d_payload;
+        switch (lanes) {
+            case 4: launch_package_fused<4>(ds, st, algo, ledger_id, d_entry_ids, d_lacs, d_length_fields, pl, payload_size, d_offsets, d_lengths, n, d_digests, err); break;
+            case 8: launch_package_fused<8>(ds, st, algo, ledger_id, d_entry_ids, d_lacs, d_length_fields, pl, payload_size, d_offsets, d_lengths, n, d_digests, err); break;
+            case 16: launch_package_fused<16>(ds, st, algo, ledger_id, d_entry_ids, d_lacs, d_length_fields, pl, payload_size, d_offsets, d_lengths, n, d_digests, err); break;
+            case 32: launch_package_fused<32>(ds, st, algo, ledger_id, d_entry_ids, d_lacs, d_length_fields, pl, payload_size, d_offsets, d_lengths, n, d_digests, err); break;
+            default: launch_package_fused<64>(ds, st, algo, ledger_id, d_entry_ids, d_lacs, d_length_fields, pl, payload_size, d_offsets, d_lengths, n, d_digests, err); break;
+        }
+        BKD_HIP(hipGetLastError());
+        hipLaunchKernelGGL(bkd::package_frame_kernel, dim3(blocks), dim3(256), 0, st, ledger_id, d_entry_ids, d_lacs,
+                           d_length_fields, d_digests, n, (uint8_t*)d_frames, frame_stride, mac);
+        BKD_HIP(hipGetLastError());
+        return BKD_OK;
+    }
     const unsigned hblocks = (unsigned)std::min<uint64_t>((n + 1023) / 1024, 2u * (uint64_t)ds.cus);
     hipLaunchKernelGGL(bkd::package_header_kernel, dim3(hblocks), dim3(1024), 0, st, tab + 1024, ledger_id, d_entry_ids,
                        d_lacs, d_length_fields, n, (uint8_t*)d_frames, frame_stride, d_digests);

@@ -464,10 +464,26 @@ __device__ __forceinline__ void stage_tables(uint32_t* lds, const uint32_t* __re
 // and short uniform entries lost (512 B +13 %, 1 KiB +2.7 %: most of their loads are tail loads,
 // profiles/r03g_ab_order*.log)
 // B16: each fold step through fold4_main (16 lookups in flight) instead of mul_main_add.
-template <int G, int PF, bool NT, bool ALIGNED, bool TAILU = BKD_TAIL_UNCOND != 0, bool B16 = false>
+// R0: the register folded into the range's first bytes — a plain value, or (LateSeed) a callable
+// evaluated only after the range's first PF + 1 loads are issued, so a chain computing it (the fused
+// package kernel's header CRC) overlaps those loads instead of delaying them.
+template <class F>
+struct LateSeed {
+    F f;
+};
+__device__ __forceinline__ uint32_t seed_value(uint32_t r0) { return r0; }
+template <class F>
+__device__ __forceinline__ uint32_t seed_value(const LateSeed<F>& r0) { return r0.f(); }
+template <class R0>
+struct IsLateSeed : std::false_type {};
+template <class F>
+struct IsLateSeed<LateSeed<F>> : std::true_type {};
+
+template <int G, int PF, bool NT, bool ALIGNED, bool TAILU = BKD_TAIL_UNCOND != 0, bool B16 = false, class R0 = uint32_t>
 __device__ __forceinline__ uint32_t fold_range(const uint32_t* lds, uint32_t lanereg, int g,
-                                               const uint8_t* __restrict__ base, int64_t s, int64_t e, uint32_t r0) {
+                                               const uint8_t* __restrict__ base, int64_t s, int64_t e, R0 r0src) {
     using Gm = Geo<G>;
+    constexpr bool kLate = IsLateSeed<R0>::value;
     const uint32_t J = (uint32_t)((e - s + Gm::kStep - 1) / Gm::kStep);
     const int64_t a = e - (int64_t)J * Gm::kStep + 16 * g;
 
@@ -481,17 +497,20 @@ __device__ __forceinline__ uint32_t fold_range(const uint32_t* lds, uint32_t lan
     } else {
         w = u32x4{0u, 0u, 0u, 0u};
     }
-    if (a < s + 4 && a + 16 > s) {
-        const int64_t d = s - a;
-        w.x ^= place_seed(r0, d);
-        w.y ^= place_seed(r0, d - 4);
-        w.z ^= place_seed(r0, d - 8);
-        w.w ^= place_seed(r0, d - 12);
-    }
     // When the range starts in the last 3 bytes of step 0's window, the tail of the seed
     // image spills into dword 0 of lane 0 at step 1; fx carries it into that first fold.
     uint32_t fx = 0u;
-    if (a + Gm::kStep < s + 4) fx = place_seed(r0, s - (a + Gm::kStep));
+    auto seed_in = [&](uint32_t r0) {
+        if (a < s + 4 && a + 16 > s) {
+            const int64_t d = s - a;
+            w.x ^= place_seed(r0, d);
+            w.y ^= place_seed(r0, d - 4);
+            w.z ^= place_seed(r0, d - 8);
+            w.w ^= place_seed(r0, d - 12);
+        }
+        if (a + Gm::kStep < s + 4) fx = place_seed(r0, s - (a + Gm::kStep));
+    };
+    if constexpr (!kLate) seed_in(seed_value(r0src));
     uint32_t c0 = w.x, c1 = w.y, c2 = w.z, c3 = w.w;
 
     // Steps 1..J-1 with PF loads in flight per lane. The steady-state loop issues its loads
@@ -526,6 +545,10 @@ __device__ __forceinline__ uint32_t fold_range(const uint32_t* lds, uint32_t lan
         u32x4 A[PF], B[PF];
 #pragma unroll
         for (int k = 0; k < PF; ++k) A[k] = ld16<NT>(p + (int64_t)k * Gm::kStep);
+        if constexpr (kLate) {  // the seed's chain runs while these loads are in flight
+            seed_in(seed_value(r0src));
+            c0 = w.x, c1 = w.y, c2 = w.z, c3 = w.w;
+        }
         p += (int64_t)PF * Gm::kStep;  // p = first step not yet loaded
         uint32_t left = rem - (uint32_t)PF;
         while (left >= 2u * PF) {
@@ -574,6 +597,10 @@ __device__ __forceinline__ uint32_t fold_range(const uint32_t* lds, uint32_t lan
         for (int k = 0; k < PF; ++k)
             if ((uint32_t)(PF + k) < left) BKD_FOLD(A[k]);
     } else {
+        if constexpr (kLate) {
+            seed_in(seed_value(r0src));
+            c0 = w.x, c1 = w.y, c2 = w.z, c3 = w.w;
+        }
         for (uint32_t k = 0; k < rem; ++k) {
             const u32x4 d = ld16<NT>(p + (int64_t)k * Gm::kStep);
             BKD_FOLD0(d);
@@ -1438,6 +1465,35 @@ __global__ void __launch_bounds__(256) package_digest_kernel(const uint32_t* __r
     put_frame_digest(frames + i * frame_stride + 32, digests[i], mac);
 }
 
+// The frames of the fused package route: each frame's 32-byte BE header (DigestManager.java:146-149)
+// and its digest at offset 32 (4-byte BE int, or 8-byte BE zero-extended long for CRC32) in one
+// pass after crc_package_fused_kernel, one frame per thread.
+__global__ void __launch_bounds__(256) package_frame_kernel(int64_t ledger_id, const int64_t* __restrict__ entry_ids,
+                                                            const int64_t* __restrict__ lacs,
+                                                            const int64_t* __restrict__ length_fields,
+                                                            const uint32_t* __restrict__ digests, uint64_t n,
+                                                            uint8_t* __restrict__ frames, uint64_t frame_stride,
+                                                            uint32_t mac) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t fld[4] = {(uint64_t)ledger_id, (uint64_t)entry_ids[i], (uint64_t)lacs[i], (uint64_t)length_fields[i]};
+    const uint32_t dg = digests[i];
+    uint32_t w[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        w[2 * k] = __builtin_bswap32((uint32_t)(fld[k] >> 32));
+        w[2 * k + 1] = __builtin_bswap32((uint32_t)fld[k]);
+    }
+    uint8_t* f = frames + i * frame_stride;
+    if ((((uintptr_t)f) & 3u) == 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) reinterpret_cast<uint32_t*>(f)[k] = w[k];
+    } else {
+        for (int k = 0; k < 32; ++k) f[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+    }
+    put_frame_digest(f + 32, dg, mac);
+}
+
 // Verify step 1 (one thread per framed entry [32 B header][mac][payload], DigestManager.java:226-283):
 // reads the header and the stored digest once — 16-byte loads when the frame is 16-byte aligned,
 // dword loads when 4-byte aligned, bytes otherwise — and writes everything step 3 needs, so that
@@ -1562,6 +1618,72 @@ __global__ void __launch_bounds__(1024) verify_gate_kernel(const uint32_t* __res
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
         out |= !PlanRun::in_band(lengths[i], ref);
     if (__any(out) && (threadIdx.x & 63) == 0) *vflag = vepoch;  // plain stores of one value: no atomics
+}
+
+// Fused package payloads (DigestManager.computeDigestAndPackageForSending, DigestManager.java:
+// 117-181): one payload per lane group. Every lane of the group builds the entry's 32-byte BE header
+// from the index arrays (ledger id, entry id, LAC, length: :146-149; one request per group per
+// field) and folds it with the x^32 operator from ~0 — update(0, header), :152 — the register the
+// payload then resumes from (:153), as crc_verify_fused_kernel does for a stored header. Only the
+// finalized digest is stored here (digests[i], a wave's groups writing consecutive words); the
+// frames' header and digest bytes are written afterwards by package_frame_kernel, so no lone frame
+// store lands between this kernel's streaming payload reads. Out-of-range payloads: digest 0 and the
+// stream's bounds flag, as the indexed path reports them.
+template <int G, int PF, bool NT>
+__global__ void __launch_bounds__(kBlock) crc_package_fused_kernel(
+    const uint8_t* __restrict__ base, uint64_t size, const uint64_t* __restrict__ offsets,
+    const uint32_t* __restrict__ lengths, uint64_t n, int64_t ledger_id, const int64_t* __restrict__ entry_ids,
+    const int64_t* __restrict__ lacs, const int64_t* __restrict__ length_fields, const uint32_t* __restrict__ tables,
+    uint32_t* __restrict__ digests, uint32_t* __restrict__ err, int sched) {
+    using Gm = Geo<G>;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[Gm::kLdsWords];
+    const uint64_t clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
+    stage_tables<G>(lds, tables);
+    const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+    const bool low_clock = lds_image_at_zero(lds) &&
+                           (sched == 2 || (sched == 0 && BKD_CLOCK_ADAPT &&
+                                           (clk1 - clk0) * 100u < (rt1 - rt0) * (uint64_t)kLowClockMHz));
+    const int lane = threadIdx.x & 63;
+    const int g = lane & (G - 1);
+    const uint32_t lanereg = ((uint32_t)(lane & 31) << 2) | (1u << 16);
+    const uint64_t ngroups = (uint64_t)gridDim.x * (kBlock / G);
+    const uint64_t gid = (uint64_t)blockIdx.x * (kBlock / G) + (uint64_t)(threadIdx.x / G);
+    for (uint64_t i = gid; i < n; i += ngroups) {
+        const uint64_t o = offsets[i];
+        const uint32_t l = lengths[i];
+        const uint64_t f4[4] = {(uint64_t)ledger_id, (uint64_t)entry_ids[i], (uint64_t)lacs[i],
+                                (uint64_t)length_fields[i]};
+        uint32_t d;
+        if (o > size || (uint64_t)l > size - o) {
+            d = 0u;
+            if (g == 0 && err) atomicOr(err, 1u);
+        } else {
+            // update(0, header): BE fields, high word first, folded by the x^32 operator from ~0 —
+            // evaluated by fold_range after the payload's first loads are issued (LateSeed)
+            auto header_reg = [&]() {
+                uint32_t reg = 0xFFFFFFFFu;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    reg = mul_aux(lds, Gm::kX32Off, reg ^ __builtin_bswap32((uint32_t)(f4[k] >> 32)));
+                    reg = mul_aux(lds, Gm::kX32Off, reg ^ __builtin_bswap32((uint32_t)f4[k]));
+                }
+                return reg;
+            };
+            uint32_t v;
+            if (l < 16u) {  // short payload: serial bytes (ReflectedIntCrc.java:44-48 form)
+                v = header_reg();
+                for (const uint8_t* q = base + o; q < base + o + l; ++q)
+                    v = lds_word(lds, Gm::kByteTabOff + (((v ^ *q) & 0xffu) << 2)) ^ (v >> 8);
+            } else {
+                const int64_t s = (int64_t)o, e = s + (int64_t)l;
+                const LateSeed<decltype(header_reg)> late{header_reg};
+                v = low_clock ? fold_range<G, PF, NT, false, BKD_TAIL_UNCOND != 0, true>(lds, lanereg, g, base, s, e, late)
+                              : fold_range<G, PF, NT, false, BKD_TAIL_UNCOND != 0, false>(lds, lanereg, g, base, s, e, late);
+            }
+            d = ~v;
+        }
+        if (g == 0) digests[i] = d;
+    }
 }
 
 template <int G, int PF, bool NT>

@@ -440,6 +440,46 @@ def test_package_batch_frame_strides(gpu, dtype, algo, stride):
 
 
 @pytest.mark.parametrize("dtype,algo", [(dg.DigestType.CRC32C, ck.CRC32C), (dg.DigestType.CRC32, ck.CRC32)])
+def test_package_in_place_and_apart_routes_agree(gpu, dtype, algo):
+    """bkd_digest_package_batch with the frames written in front of their own payloads (one buffer:
+    the header-first route) and into a buffer of their own (the fused route): the same digests, and
+    frame bytes equal to the oracle's in both, the in-place payloads untouched."""
+    import ctypes
+    import torch
+    n, L = 4096, 4096
+    mac = 4 if algo == ck.CRC32C else 8
+    hl = 32 + mac
+    plen = L - hl
+    raw = oracle.fill_splitmix64(n * L, 61)
+    ids = np.arange(n, dtype=np.int64) + 9
+    buf = _dev_bytes(torch, raw, gpu)
+    d_ids, d_lacs = torch.from_numpy(ids).to(gpu), torch.from_numpy(ids - 1).to(gpu)
+    d_lenf = torch.full((n,), plen, dtype=torch.int64, device=gpu)
+    d_off = torch.from_numpy(np.arange(n, dtype=np.int64) * L + hl).to(gpu)
+    d_len = torch.full((n,), plen, dtype=torch.int32, device=gpu)
+    apart = torch.empty(n * hl, dtype=torch.uint8, device=gpu)
+    dig_a = torch.empty(n, dtype=torch.int32, device=gpu)
+    dig_b = torch.empty(n, dtype=torch.int32, device=gpu)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    for frames, stride, dig in ((apart, hl, dig_a), (buf, L, dig_b)):
+        ck._native.check(ck.lib().bkd_digest_package_batch(algo, 3, p(d_ids), p(d_lacs), p(d_lenf), p(buf), buf.numel(),
+                                                           p(d_off), p(d_len), n, p(frames), stride, p(dig), None))
+    torch.cuda.synchronize()
+    assert torch.equal(dig_a, dig_b)
+    digs = dig_a.cpu().numpy().view(np.uint32)
+    got_apart = apart.cpu().numpy().reshape(n, hl)
+    got_buf = buf.cpu().numpy().reshape(n, L)
+    for i in range(n):
+        pay = raw[i * L + hl:(i + 1) * L]
+        d, hdr = oracle.digest_entry(algo, 3, int(ids[i]), int(ids[i]) - 1, plen, pay)
+        assert digs[i] == d, i
+        want = hdr + oracle.digest_bytes(algo, d)
+        assert got_apart[i].tobytes() == want, i
+        assert got_buf[i, :hl].tobytes() == want, i
+        assert got_buf[i, hl:].tobytes() == pay.tobytes(), i
+
+
+@pytest.mark.parametrize("dtype,algo", [(dg.DigestType.CRC32C, ck.CRC32C), (dg.DigestType.CRC32, ck.CRC32)])
 @pytest.mark.parametrize("skip", [False, True])
 def test_verify_batch_near_uniform_frames(gpu, dtype, algo, skip):
     """Frames whose lengths all lie in the near-uniform band take the fused verify (gate -> one kernel

@@ -137,6 +137,14 @@ def main(paths):
         if name == "package4k":
             framed()
             return package(L)
+        if name == "package4k_sep":  # frames into their own packed buffer (stride 32 + mac), as bench.py
+            framed()
+            f = fr
+            if "sep" not in f:
+                f["sep"] = torch.empty(n * 36, dtype=torch.uint8, device=dev)
+            return L.bkd_digest_package_batch(0, 7, ptr(f["ids"]), ptr(f["lacs"]), ptr(f["lenf"]), ptr(f["F"]),
+                                              f["F"].numel(), ptr(f["poff"]), ptr(f["plen"]), n, ptr(f["sep"]), 36,
+                                              ptr(f["dig"]), ctypes.c_void_p(st.cuda_stream))
         if name == "verify4k":
             f = framed()
             r = L.bkd_digest_verify_batch(0, 7, 0, 0, ptr(f["F"]), f["F"].numel(), ptr(f["foff"]), ptr(f["flen"]), n,
@@ -165,8 +173,8 @@ def main(paths):
             assert call(L, name) == 0, name
             torch.cuda.synchronize()
             cnt = work[name][1].numel() if name in work else ((4 << 30) // small[name][0] if name in small else n)
-            if name in ("package4k", "verify4k"):
-                out[:n].copy_(fr["dig"] if name == "package4k" else fr["status"])
+            if name in ("package4k", "package4k_sep", "verify4k"):
+                out[:n].copy_(fr["status"] if name == "verify4k" else fr["dig"])
             if ref is None:
                 ref = out[:cnt].clone()
             if not os.environ.get("AB_NOCHECK"):  # (measurement-only variants compute wrong digests)

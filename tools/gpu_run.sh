@@ -12,6 +12,8 @@
 #   verify | shard8m bench.py --config verify4k | shard8m
 #   stats_uniform | stats_zipf   rocprofv3 --kernel-trace --stats of the driver's command / zipf
 #   pmc_uniform | pmc_zipf       FETCH_SIZE and WRITE_SIZE passes (separate) + tools/pmc_summary.py
+#   pmc_verify | pmc_package     the same for bench.py --config verify4k --digest-op verify | package
+#   stats_verify | stats_package rocprofv3 --kernel-trace --stats of one framed route
 #   ab:LIBS          tools/ab_libs.py over the comma-separated libs (AB_WORK selects workloads)
 #   kstats:LIB       rocprofv3 kernel stats of tools/ab_libs.py on one library (AB_WORK workloads)
 #   py:SCRIPT        python3 SCRIPT (a tools/ diagnostic)
@@ -47,6 +49,19 @@ for step in "$@"; do
        run pmc_write_$cfg 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write_$cfg -o pmc -- python3 $R/bench.py $extra --steps 5 --warmup 1) || exit 1
       if [ $cfg = zipf ]; then zipf_bytes; python3 tools/pmc_summary.py $O/pmc_fetch_zipf $O/pmc_write_zipf zipf $ZB bkd::crc_plan_chunks_kernel > $O/pmc_z.json || exit 1
       else python3 tools/pmc_summary.py $O/pmc_fetch_uniform $O/pmc_write_uniform uniform4k $((1048576*4100)) > $O/pmc_u.json || exit 1; fi ;;
+    pmc_verify|pmc_package)  # the framed routes on their own: --digest-op verify | package
+      op=${step#pmc_}; cfg=${op}4k
+      # other kernels: the measured call's own launches (each bench also runs the other route once)
+      if [ $op = verify ]; then mk=bkd::crc_verify_fused_kernel; ab=$((1048576*(4096+12+4)))
+        ok=bkd::verify_gate_kernel,bkd::verify_header_kernel,bkd::plan_count_kernel,bkd::plan_scan_kernel,bkd::plan_emit_kernel,bkd::crc_plan_chunks_kernel,bkd::plan_combine_kernel,bkd::verify_finish_kernel
+      else mk=bkd::crc_package_fused_kernel; ab=$((1048576*(4060+24+12+36+4))); ok=bkd::package_frame_kernel; fi
+      (cd /tmp && export TMPDIR=/tmp &&
+       run pmc_fetch_$cfg 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_$cfg -o pmc -- python3 $R/bench.py --config verify4k --digest-op $op --steps 5 --warmup 1 &&
+       run pmc_write_$cfg 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write_$cfg -o pmc -- python3 $R/bench.py --config verify4k --digest-op $op --steps 5 --warmup 1) || exit 1
+      python3 tools/pmc_summary.py $O/pmc_fetch_$cfg $O/pmc_write_$cfg $cfg $ab $mk $ok > $O/pmc_$cfg.json || exit 1 ;;
+    stats_verify|stats_package)
+      op=${step#stats_}
+      (cd /tmp && export TMPDIR=/tmp && run stats_$op 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$op -o $op -- python3 $R/bench.py --config verify4k --digest-op $op --steps 20 --warmup 5) || exit 1 ;;
     ab:*) run ab_$(date +%s%N) 900 python3 tools/ab_libs.py $(echo ${step#ab:} | tr , " ") ;;
     kstats:*) lib=${step#kstats:}; nm=$(basename $lib .so); (cd /tmp && export TMPDIR=/tmp && AB_ROUNDS=${AB_ROUNDS:-2} run kstats_$nm 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kstats_$nm -o k -- python3 $R/tools/ab_libs.py $R/$lib) || exit 1
       python3 tools/kstats.py $O/kstats_$nm > $O/kstats_$nm.txt && cat $O/kstats_$nm.txt ;;
