@@ -1,11 +1,12 @@
 """Summarise rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) into profiles/pmc_<config>.json.
 
 gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports half the bytes of a wide
-coalesced streaming read, so read bytes = 2 * FETCH_SIZE * 1024 for the streaming CRC kernels
-(crc_groups_kernel, crc_plan_chunks_kernel); WRITE_SIZE is exact for 16 B/lane streaming stores
-(the 4 B/lane digest stores are uncalibrated and a small share of the traffic). The plan's small
-index/descriptor kernels (plan_*) are reported separately, raw (no correction: their accesses are
-not wide streaming reads).
+coalesced streaming read, so read bytes = 2 * FETCH_SIZE * 1024. The same half count holds for the
+small kernels' coalesced 4- and 8-byte loads: calibrated on package_frame_kernel, which reads exactly
+28 B per entry (three int64 index fields and a u32 digest) and reports 14 350 kB per 1M entries =
+0.50 of 29.4 MB (round 5, profiles/pmc_package4k.json). So every kernel's reads are doubled.
+WRITE_SIZE is exact for 16 B/lane streaming stores (the frame kernel's 36-byte frame stores read
+1.057 x their bytes). The other kernels of the call are reported beside the main one.
 
 Each summary carries lib_sha256, the sha256 of the bookkeeper_amd/libbkdigest.so the counters were
 collected on.
@@ -56,18 +57,19 @@ def main(fetch_dir, write_dir, config, algo_bytes, main_kernel="bkd::crc_groups_
     for k in sorted(set(f) | set(w)):
         if k == main_kernel or (keep is not None and k not in keep):
             continue
-        aux[k] = {"FETCH_SIZE_kB_median_raw": median(f[k]["FETCH_SIZE"]),
+        aux[k] = {"FETCH_SIZE_kB_median": median(f[k]["FETCH_SIZE"]),
                   "WRITE_SIZE_kB_median": median(w[k]["WRITE_SIZE"])}
-    aux_b = sum((a["FETCH_SIZE_kB_median_raw"] + a["WRITE_SIZE_kB_median"]) * 1024 for a in aux.values())
+    aux_b = sum((2 * a["FETCH_SIZE_kB_median"] + a["WRITE_SIZE_kB_median"]) * 1024 for a in aux.values())
     out = {"config": config, "kernel": main_kernel, "dispatches": len(f[main_kernel]["FETCH_SIZE"]),
            "FETCH_SIZE_kB_median": fetch_kb, "WRITE_SIZE_kB_median": write_kb,
            "hbm_read_bytes_per_launch": read_b, "hbm_write_bytes_per_launch": write_b,
            "hbm_bytes_per_launch": read_b + write_b + aux_b, "main_kernel_bytes_per_launch": read_b + write_b,
-           "other_kernels": aux, "other_kernels_bytes_per_launch_raw": aux_b,
+           "other_kernels": aux, "other_kernels_bytes_per_launch": aux_b,
            "algorithmic_bytes_per_launch": algo_bytes,
            "traffic_over_algorithmic": (read_b + write_b + aux_b) / algo_bytes,
-           "correction": "main kernel: read = 2 x FETCH_SIZE x 1024 (gfx950 half-count of wide streaming reads), "
-                         "write = WRITE_SIZE x 1024; other kernels raw",
+           "correction": "every kernel: read = 2 x FETCH_SIZE x 1024 (gfx950 half count of coalesced reads, "
+                         "calibrated on 16-B streaming loads and on package_frame_kernel's 4/8-B loads), "
+                         "write = WRITE_SIZE x 1024",
            # provenance: the build these counters came from (bench.py attaches `traffic` only when the
            # library it times has this hash)
            "lib_sha256": hashlib.sha256(open(LIB, "rb").read()).hexdigest(),
