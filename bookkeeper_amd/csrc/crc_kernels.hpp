@@ -648,6 +648,75 @@ __device__ __forceinline__ void groups_loop(const uint32_t* lds, uint32_t lanere
     }
 }
 
+// Held result stores. A result store inside the load stream costs in proportion to the bytes it
+// writes, whatever its grouping or place: a uniform-kernel build without result stores ran 2.5–2.9 %
+// faster, one storing a round in eight 1.8–2.5 % faster, while coalescing each wave's words into one
+// 256-byte store, storing one entry late or nontemporal stores gained nothing (profiles/r06ac_ag_*).
+// So a group's result of round r (item gid + r·ngroups) moves to lane r mod G of the group
+// (ds_bpermute from the group's lane 0) and stays in a register until K·G rounds are held; then
+// every lane stores its K words at once, and the rest when the group's loop ends.
+#ifndef BKD_HOLD_STORE
+#define BKD_HOLD_STORE 8  // K: words held per lane (0: each round stores its result)
+#endif
+template <int G, int K>
+struct HeldResults {
+    uint32_t hold[K];
+    uint64_t r0 = 0;  // first round held
+    int k = 0, sub = 0;  // slot and lane of the next round (the same in every lane of the group)
+    __device__ __forceinline__ HeldResults() {
+#pragma unroll
+        for (int q = 0; q < K; ++q) hold[q] = 0u;
+    }
+    __device__ __forceinline__ void flush(int kmax, int g, uint32_t* __restrict__ out, uint64_t gid, uint64_t ngroups,
+                                          uint64_t n) const {
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            const uint64_t i = gid + (r0 + (uint64_t)q * G + (uint64_t)g) * ngroups;
+            if (q < kmax && i < n) out[i] = hold[q];
+        }
+    }
+    // v: this round's result, valid in the group's lane 0 (every lane of the group calls)
+    __device__ __forceinline__ void put(uint32_t v, int g, uint32_t* __restrict__ out, uint64_t gid, uint64_t ngroups,
+                                        uint64_t n) {
+        const int from = ((int)(threadIdx.x & 63) & ~(G - 1)) << 2;
+        const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(from, (int)v);
+#pragma unroll
+        for (int q = 0; q < K; ++q)
+            if (q == k && g == sub) hold[q] = b;
+        if (++sub == G) {
+            sub = 0;
+            if (++k == K) {
+                flush(K, g, out, gid, ngroups, n);
+                r0 += (uint64_t)K * G;
+                k = 0;
+            }
+        }
+    }
+    // after the group's last round: slots below k are full, slot k holds lanes 0 .. sub-1 (the lanes
+    // past them hold rounds at or after the one that ended the loop: items >= n, not stored)
+    __device__ __forceinline__ void finish(int g, uint32_t* __restrict__ out, uint64_t gid, uint64_t ngroups,
+                                           uint64_t n) const {
+        flush(sub > 0 ? k + 1 : k, g, out, gid, ngroups, n);
+    }
+};
+
+// Long uniform entries (>= 16 B, 32 steps or more: no serial or out-of-range items) with held stores.
+template <int G, int PF, bool NT, int K>
+__device__ __forceinline__ void held_store_loop(const uint32_t* lds, uint32_t lanereg, int g,
+                                                const uint8_t* __restrict__ base, const UniformSrc& src, uint64_t n,
+                                                uint64_t gid, uint64_t ngroups, bool low_clock) {
+    HeldResults<G, K> held;
+    for (uint64_t i = gid; i < n; i += ngroups) {
+        Work wk;
+        src.get(i, wk);
+        const uint32_t v =
+            low_clock ? fold_range<G, PF, NT, false, true, true>(lds, lanereg, g, base, wk.s, wk.s + (int64_t)wk.len, wk.r0)
+                      : fold_range<G, PF, NT, false, true, false>(lds, lanereg, g, base, wk.s, wk.s + (int64_t)wk.len, wk.r0);
+        held.put(v ^ wk.xorout, g, src.out, gid, ngroups, n);
+    }
+    held.finish(g, src.out, gid, ngroups, n);
+}
+
 // Uniform batches of short entries (16 B <= len <= 16*G*(PF+1), every load of an entry fits one
 // register set): a group's next entry is loaded while the current one folds (X/Y register sets),
 // so a wave no longer waits one HBM round trip per entry — the one-entry-per-group loop is
@@ -937,6 +1006,9 @@ __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __res
             else saw = indexed_small_loop<G, PF, NT, false>(lds, lanereg, g, base, src, n, gid, ngroups, err);
         }
         if (__any(saw) && (threadIdx.x & 63) == 0 && src.plan_flag) *src.plan_flag = src.plan_epoch;
+    } else if constexpr (std::is_same<Src, UniformLongSrc>::value && BKD_HOLD_STORE > 0) {
+        // (long uniform entries >= 16 B: no serial or out-of-range items)
+        if (gid < n) held_store_loop<G, PF, NT, BKD_HOLD_STORE>(lds, lanereg, g, base, src, n, gid, ngroups, low_clock);
     } else {
         groups_loop<G, PF, NT>(lds, lanereg, g, base, src, n, gid, ngroups, err, low_clock);
     }
@@ -1648,6 +1720,9 @@ __global__ void __launch_bounds__(kBlock) crc_package_fused_kernel(
     const uint32_t lanereg = ((uint32_t)(lane & 31) << 2) | (1u << 16);
     const uint64_t ngroups = (uint64_t)gridDim.x * (kBlock / G);
     const uint64_t gid = (uint64_t)blockIdx.x * (kBlock / G) + (uint64_t)(threadIdx.x / G);
+#if BKD_HOLD_STORE > 0
+    HeldResults<G, BKD_HOLD_STORE> held;
+#endif
     for (uint64_t i = gid; i < n; i += ngroups) {
         const uint64_t o = offsets[i];
         const uint32_t l = lengths[i];
@@ -1682,8 +1757,15 @@ __global__ void __launch_bounds__(kBlock) crc_package_fused_kernel(
             }
             d = ~v;
         }
+#if BKD_HOLD_STORE > 0
+        held.put(d, g, digests, gid, ngroups, n);
+#else
         if (g == 0) digests[i] = d;
+#endif
     }
+#if BKD_HOLD_STORE > 0
+    held.finish(g, digests, gid, ngroups, n);
+#endif
 }
 
 template <int G, int PF, bool NT>
@@ -1707,6 +1789,9 @@ __global__ void __launch_bounds__(kBlock) crc_verify_fused_kernel(
     const uint32_t lanereg = ((uint32_t)(lane & 31) << 2) | (1u << 16);
     const uint64_t ngroups = (uint64_t)gridDim.x * (kBlock / G);
     const uint64_t gid = (uint64_t)blockIdx.x * (kBlock / G) + (uint64_t)(threadIdx.x / G);
+#if BKD_HOLD_STORE > 0
+    HeldResults<G, BKD_HOLD_STORE> held;
+#endif
     for (uint64_t i = gid; i < n; i += ngroups) {
         const uint64_t o = offsets[i];
         const uint32_t l = lengths[i];
@@ -1749,11 +1834,19 @@ __global__ void __launch_bounds__(kBlock) crc_verify_fused_kernel(
             else if (id_checks == 0 && eid != first_entry_id + (int64_t)i) st = 4;
             else st = 0;
         }
+#if BKD_HOLD_STORE > 0
+        held.put((uint32_t)st, g, reinterpret_cast<uint32_t*>(status), gid, ngroups, n);
+        if (g == 0 && st != 0) atomicMin(first_bad, (unsigned long long)i);
+#else
         if (g == 0) {
             status[i] = st;
             if (st != 0) atomicMin(first_bad, (unsigned long long)i);
         }
+#endif
     }
+#if BKD_HOLD_STORE > 0
+    held.finish(g, reinterpret_cast<uint32_t*>(status), gid, ngroups, n);
+#endif
 }
 
 }  // namespace bkd

@@ -146,6 +146,38 @@ def test_uniform_batches(gpu, algo, lanes):
         assert (got.cpu().numpy().view(np.uint32) == want).all(), (entry_len, stride, n)
 
 
+@pytest.mark.parametrize("algo", [ck.CRC32C, ck.CRC32])
+def test_uniform_long_held_stores_round_boundaries(gpu, algo):
+    """Long uniform entries (8-lane groups, >= 32 steps) keep each group's results in its lanes and
+    store them every 8 x 8 rounds and at the end (held_store_loop): batch sizes around the grid
+    (one group, a partial first round, exactly one round, one past it, several rounds with a partial
+    last one), per-entry seeds and a common seed, unaligned strides; every digest equals the oracle's."""
+    import torch
+    cus = torch.cuda.get_device_properties(gpu).multi_processor_count
+    ngroups = cus * (1024 // 8)
+    ck.set_group_lanes(8)
+    try:
+        for entry_len, stride, n in [(4096, 4096, 1), (4096, 4096, ngroups - 1), (4096, 4096, ngroups),
+                                     (4096, 4096, ngroups + 1), (5000, 5004, 3 * ngroups + 77),
+                                     (4096, 4096, 9 * ngroups + 5)]:
+            nbytes = (n - 1) * stride + entry_len
+            data = oracle.fill_splitmix64(nbytes, 7 + n)
+            base = _dev_bytes(torch, data, gpu)
+            got = ck.crc_batch_uniform(algo, base, entry_len, n, stride=stride, seed_all=0x5EED)
+            want = oracle.uniform(algo, data, stride, entry_len, n, 0x5EED)
+            assert (got.cpu().numpy().view(np.uint32) == want).all(), (entry_len, stride, n)
+            if n <= ngroups + 1:
+                seeds = np.random.default_rng(n).integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+                got = ck.crc_batch_uniform(algo, base, entry_len, n, stride=stride,
+                                           seeds=torch.from_numpy(seeds.view(np.int32)).to(gpu))
+                offs = np.arange(n, dtype=np.uint64) * stride
+                want = oracle.batch(algo, data, offs, np.full(n, entry_len, dtype=np.uint32), seeds)
+                assert (got.cpu().numpy().view(np.uint32) == want).all(), ("seeds", n)
+            del base
+    finally:
+        ck.set_group_lanes(0)
+
+
 @pytest.mark.parametrize("lanes", LANES)
 def test_uniform_short_entries_seeded(gpu, lanes):
     """Short uniform entries take the pipelined short-entry loop (every load of an entry in one
