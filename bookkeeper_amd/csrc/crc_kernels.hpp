@@ -658,45 +658,54 @@ __device__ __forceinline__ void groups_loop(const uint32_t* lds, uint32_t lanere
 #ifndef BKD_HOLD_STORE
 #define BKD_HOLD_STORE 8  // K: words held per lane (0: each round stores its result)
 #endif
+
+constexpr int kHoldLong = 32;  // words held per lane in the uniform kernel for batches of > 8·G rounds
+
 template <int G, int K>
 struct HeldResults {
     uint32_t hold[K];
-    uint64_t r0 = 0;  // first round held
+    uint32_t cur = 0u;   // the slot being filled: lane g takes round r0 + k·G + g
+    uint64_t r0 = 0;     // first round held
     int k = 0, sub = 0;  // slot and lane of the next round (the same in every lane of the group)
     __device__ __forceinline__ HeldResults() {
 #pragma unroll
         for (int q = 0; q < K; ++q) hold[q] = 0u;
     }
-    __device__ __forceinline__ void flush(int kmax, int g, uint32_t* __restrict__ out, uint64_t gid, uint64_t ngroups,
-                                          uint64_t n) const {
+    // slots q < kfull from hold[], then slot kfull from cur when `partial`
+    __device__ __forceinline__ void flush(int kfull, bool partial, int g, uint32_t* __restrict__ out, uint64_t gid,
+                                          uint64_t ngroups, uint64_t n) const {
 #pragma unroll
         for (int q = 0; q < K; ++q) {
             const uint64_t i = gid + (r0 + (uint64_t)q * G + (uint64_t)g) * ngroups;
-            if (q < kmax && i < n) out[i] = hold[q];
+            if (q < kfull && i < n) out[i] = hold[q];
         }
+        const uint64_t i = gid + (r0 + (uint64_t)kfull * G + (uint64_t)g) * ngroups;
+        if (partial && i < n) out[i] = cur;
     }
-    // v: this round's result, valid in the group's lane 0 (every lane of the group calls)
+    // v: this round's result, valid in the group's lane 0 (every lane of the group calls). One select
+    // per round; the slot is filed into hold[] (a chain of K selects: the index is not static) once
+    // every G rounds.
     __device__ __forceinline__ void put(uint32_t v, int g, uint32_t* __restrict__ out, uint64_t gid, uint64_t ngroups,
                                         uint64_t n) {
         const int from = ((int)(threadIdx.x & 63) & ~(G - 1)) << 2;
         const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(from, (int)v);
-#pragma unroll
-        for (int q = 0; q < K; ++q)
-            if (q == k && g == sub) hold[q] = b;
+        cur = g == sub ? b : cur;
         if (++sub == G) {
             sub = 0;
+#pragma unroll
+            for (int q = 0; q < K; ++q) hold[q] = q == k ? cur : hold[q];  // selects: no indexed (scratch) array
             if (++k == K) {
-                flush(K, g, out, gid, ngroups, n);
+                flush(K, false, g, out, gid, ngroups, n);
                 r0 += (uint64_t)K * G;
                 k = 0;
             }
         }
     }
-    // after the group's last round: slots below k are full, slot k holds lanes 0 .. sub-1 (the lanes
-    // past them hold rounds at or after the one that ended the loop: items >= n, not stored)
+    // after the group's last round: slots below k are full, `cur` holds lanes 0 .. sub-1 of slot k
+    // (the lanes past them hold rounds at or after the one that ended the loop: items >= n, not stored)
     __device__ __forceinline__ void finish(int g, uint32_t* __restrict__ out, uint64_t gid, uint64_t ngroups,
                                            uint64_t n) const {
-        flush(sub > 0 ? k + 1 : k, g, out, gid, ngroups, n);
+        flush(k, sub > 0, g, out, gid, ngroups, n);
     }
 };
 
@@ -1008,7 +1017,15 @@ __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __res
         if (__any(saw) && (threadIdx.x & 63) == 0 && src.plan_flag) *src.plan_flag = src.plan_epoch;
     } else if constexpr (std::is_same<Src, UniformLongSrc>::value && BKD_HOLD_STORE > 0) {
         // (long uniform entries >= 16 B: no serial or out-of-range items)
-        if (gid < n) held_store_loop<G, PF, NT, BKD_HOLD_STORE>(lds, lanereg, g, base, src, n, gid, ngroups, low_clock);
+        // K = 8 holds a group's 64 rounds (1M entries at 32 768 groups: 32); larger batches hold 32
+        // words per lane so that they too store only at the end (8M: 256 rounds, -1.5 %; K = 32 for
+        // 1M entries measured +0.3 to +0.8 %, profiles/r06aq_*, r06ar_*)
+        if (gid < n) {
+            if ((n + ngroups - 1) / ngroups <= (uint64_t)BKD_HOLD_STORE * G)
+                held_store_loop<G, PF, NT, BKD_HOLD_STORE>(lds, lanereg, g, base, src, n, gid, ngroups, low_clock);
+            else
+                held_store_loop<G, PF, NT, kHoldLong>(lds, lanereg, g, base, src, n, gid, ngroups, low_clock);
+        }
     } else {
         groups_loop<G, PF, NT>(lds, lanereg, g, base, src, n, gid, ngroups, err, low_clock);
     }

@@ -111,6 +111,7 @@ def main(paths):
     assert base.numel() >= 4 << 30
 
     fr = {}
+    big = {}  # uniform4k_8m's 32 GiB shard
 
     def framed():  # 1M framed 4 KiB entries (CRC32C: 32 B header + 4 B digest + payload), packaged once
         if not fr:
@@ -150,6 +151,14 @@ def main(paths):
             r = L.bkd_digest_verify_batch(0, 7, 0, 0, ptr(f["F"]), f["F"].numel(), ptr(f["foff"]), ptr(f["flen"]), n,
                                           ptr(f["status"]), ptr(f["fb"]), ctypes.c_void_p(st.cuda_stream))
             return r
+        if name == "uniform4k_8m":  # config 4's per-GPU shard: 8M x 4 KiB (32 GiB, contents as allocated)
+            if "big8m" not in big:
+                big["big8m"] = torch.empty(8 * n * 4096, dtype=torch.uint8, device=dev)
+                big["out8m"] = torch.empty(8 * n, dtype=torch.int32, device=dev)
+            L.bkd_set_group_lanes(0)
+            r = L.bkd_crc_batch_uniform(0, ptr(big["big8m"]), 4096, 4096, 8 * n, None, 0, ptr(big["out8m"]),
+                                        ctypes.c_void_p(st.cuda_stream))
+            return r
         if name == "uniform4k":
             L.bkd_set_group_lanes(0)
             return L.bkd_crc_batch_uniform(0, ptr(base), 4096, 4096, n, None, 0, ptr(out), ctypes.c_void_p(st.cuda_stream))
@@ -175,6 +184,8 @@ def main(paths):
             cnt = work[name][1].numel() if name in work else ((4 << 30) // small[name][0] if name in small else n)
             if name in ("package4k", "package4k_sep", "verify4k"):
                 out[:n].copy_(fr["status"] if name == "verify4k" else fr["dig"])
+            if name == "uniform4k_8m":  # the shard's last 1M digests (its last flushes)
+                out[:n].copy_(big["out8m"][-n:])
             if ref is None:
                 ref = out[:cnt].clone()
             if not os.environ.get("AB_NOCHECK"):  # (measurement-only variants compute wrong digests)
@@ -191,7 +202,8 @@ def main(paths):
                 e1.record(st)
                 torch.cuda.synchronize()
                 res.setdefault((name, lname), []).append(e0.elapsed_time(e1) / REPS)
-        nbytes = work[name][3] if name in work else (4 << 30 if name in small else n * 4096)
+        nbytes = work[name][3] if name in work else (4 << 30 if name in small else
+                                                     8 * n * 4096 if name == "uniform4k_8m" else n * 4096)
         for lname in libs:
             v = sorted(res[(name, lname)])
             print(f"{name:12s} {lname:22s} median {v[len(v) // 2]:.4f} ms  min {v[0]:.4f} ms  "
