@@ -709,8 +709,9 @@ struct HeldResults {
     }
 };
 
-// Long uniform entries (>= 16 B, 32 steps or more: no serial or out-of-range items) with held stores.
-template <int G, int PF, bool NT, int K>
+// Uniform entries (>= 16 B: no serial or out-of-range items) with held stores; TAILU as the kernel
+// would fold them (unconditional tail loads for UniformLongSrc's 32 steps or more).
+template <int G, int PF, bool NT, int K, bool TAILU = true>
 __device__ __forceinline__ void held_store_loop(const uint32_t* lds, uint32_t lanereg, int g,
                                                 const uint8_t* __restrict__ base, const UniformSrc& src, uint64_t n,
                                                 uint64_t gid, uint64_t ngroups, bool low_clock) {
@@ -719,8 +720,8 @@ __device__ __forceinline__ void held_store_loop(const uint32_t* lds, uint32_t la
         Work wk;
         src.get(i, wk);
         const uint32_t v =
-            low_clock ? fold_range<G, PF, NT, false, true, true>(lds, lanereg, g, base, wk.s, wk.s + (int64_t)wk.len, wk.r0)
-                      : fold_range<G, PF, NT, false, true, false>(lds, lanereg, g, base, wk.s, wk.s + (int64_t)wk.len, wk.r0);
+            low_clock ? fold_range<G, PF, NT, false, TAILU, true>(lds, lanereg, g, base, wk.s, wk.s + (int64_t)wk.len, wk.r0)
+                      : fold_range<G, PF, NT, false, TAILU, false>(lds, lanereg, g, base, wk.s, wk.s + (int64_t)wk.len, wk.r0);
         held.put(v ^ wk.xorout, g, src.out, gid, ngroups, n);
     }
     held.finish(g, src.out, gid, ngroups, n);
@@ -1004,6 +1005,18 @@ __global__ void __launch_bounds__(kBlock) crc_groups_kernel(const uint8_t* __res
             if (gid < n) {
                 if (src.seeds) uniform_small_loop<G, PF, NT, true>(lds, lanereg, g, base, src, n, gid, ngroups);
                 else uniform_small_loop<G, PF, NT, false>(lds, lanereg, g, base, src, n, gid, ngroups);
+            }
+            return;
+        }
+        // entries past the short loop and below UniformLongSrc's 32 steps, results held as there:
+        // 512 B -11 %, 1 KiB -7 %, 2 KiB -6 % (8-lane groups; profiles/r06aw_ax_*). (Held in the
+        // short loop itself they cost 2-5 %: its entries are a few folds each.)
+        if (BKD_HOLD_STORE > 0 && src.len >= 16u) {
+            if (gid < n) {
+                if ((n + ngroups - 1) / ngroups <= (uint64_t)BKD_HOLD_STORE * G)
+                    held_store_loop<G, PF, NT, BKD_HOLD_STORE, BKD_TAIL_UNCOND != 0>(lds, lanereg, g, base, src, n, gid, ngroups, low_clock);
+                else
+                    held_store_loop<G, PF, NT, kHoldLong, BKD_TAIL_UNCOND != 0>(lds, lanereg, g, base, src, n, gid, ngroups, low_clock);
             }
             return;
         }
