@@ -659,6 +659,9 @@ __device__ __forceinline__ void groups_loop(const uint32_t* lds, uint32_t lanere
 #define BKD_HOLD_STORE 8  // K: words held per lane (0: each round stores its result)
 #endif
 
+#ifndef BKD_HOLD_SHORT
+#define BKD_HOLD_SHORT 2  // the chunk kernel's short tail: K·G = 16 rounds per group (config 3: ~15)
+#endif
 constexpr int kHoldLong = 32;  // words held per lane in the uniform kernel for batches of > 8·G rounds
 
 template <int G, int K>
@@ -1318,7 +1321,13 @@ template <int G, int PF, bool NT>
 __device__ __forceinline__ void short_chunks_loop(const uint32_t* lds, uint32_t lanereg, int g,
                                                   const uint8_t* __restrict__ base, const PlanDesc* __restrict__ descs,
                                                   uint64_t i, uint64_t n, uint64_t ngroups, uint32_t* __restrict__ out,
-                                                  uint32_t* __restrict__ partials) {
+                                                  uint32_t* __restrict__ partials, uint64_t nstart) {
+#if BKD_HOLD_SHORT > 0
+    // partials by list position, held (HeldResults; a final chunk's or a hole's word lands in its own
+    // unused slot): the short tail is a group's last work, so they are stored at its very end
+    const uint64_t gid0 = i - nstart;
+    HeldResults<G, BKD_HOLD_SHORT> held;
+#endif
     auto clampi = [&](uint64_t j) { return j < n ? j : n - 1; };
     auto geo_at = [&](uint64_t j) {
         ChunkGeo c = chunk_geo<G>(descs[clampi(j)], g);
@@ -1349,13 +1358,21 @@ __device__ __forceinline__ void short_chunks_loop(const uint32_t* lds, uint32_t 
     load(cz, W0z, Az);
     PlanDesc dx = descs[clampi(i + 3 * ngroups)], dy = descs[clampi(i + 4 * ngroups)],
              dz = descs[clampi(i + 5 * ngroups)];
+#if BKD_HOLD_SHORT > 0
+#define BKD_SHORT_EMIT(C, v)                                                                 \
+    held.put(v, g, partials + nstart, gid0, ngroups, n - nstart);                            \
+    if (g == 0 && C.len && (C.dst & kPlanFinal)) out[C.dst & ~kPlanFinal] = ~v;
+#else
+#define BKD_SHORT_EMIT(C, v)                                                                 \
+    if (g == 0 && C.len) {                                                                   \
+        if (C.dst & kPlanFinal) out[C.dst & ~kPlanFinal] = ~v;                               \
+        else partials[C.dst] = v;                                                            \
+    }
+#endif
 #define BKD_SHORT_STEP(C, W0C, AC, DC)                                                       \
     {                                                                                        \
         const uint32_t v = C.len ? short_chunk_fold<G, PF>(lds, lanereg, C, W0C, AC) : 0u;   \
-        if (g == 0 && C.len) {                                                               \
-            if (C.dst & kPlanFinal) out[C.dst & ~kPlanFinal] = ~v;                           \
-            else partials[C.dst] = v;                                                        \
-        }                                                                                    \
+        BKD_SHORT_EMIT(C, v)                                                                 \
         C = chunk_geo<G>(DC, g); /* chunk i + 3 ngroups */                                   \
         if (i + 3 * ngroups >= n) C.len = 0;                                                 \
         load(C, W0C, AC);                                                                    \
@@ -1371,6 +1388,10 @@ __device__ __forceinline__ void short_chunks_loop(const uint32_t* lds, uint32_t 
         BKD_SHORT_STEP(cz, W0z, Az, dz)
     }
 #undef BKD_SHORT_STEP
+#undef BKD_SHORT_EMIT
+#if BKD_HOLD_SHORT > 0
+    held.finish(g, partials + nstart, gid0, ngroups, n - nstart);
+#endif
 }
 
 // Chunks [0, n) of the list in grid stride, one prefetched chunk per group (X/Y sets).
@@ -1456,7 +1477,7 @@ __device__ __forceinline__ void plan_chunks_loop(const uint32_t* lds, uint32_t l
     if (gid < nmain) long_chunks_loop<G, PF, NT>(lds, lanereg, g, base, descs, nmain, gid, ngroups, out, partials);
     if (nmain < n && gid < n - nmain)
         short_chunks_loop<G, kShortPF, NT && BKD_SHORT_NT>(lds, lanereg, g, base, descs, nmain + gid, n, ngroups, out,
-                                                          partials);
+                                                          partials, nmain);
 }
 
 
