@@ -659,6 +659,9 @@ __device__ __forceinline__ void groups_loop(const uint32_t* lds, uint32_t lanere
 #define BKD_HOLD_STORE 8  // K: words held per lane (0: each round stores its result)
 #endif
 
+#ifndef BKD_HOLD_LONGLOOP
+#define BKD_HOLD_LONGLOOP 8  // the chunk kernel's long loop: 64 rounds per flush (config 3: ~60), 128 VGPRs
+#endif
 #ifndef BKD_HOLD_SHORT
 #define BKD_HOLD_SHORT 2  // the chunk kernel's short tail: K·G = 16 rounds per group (config 3: ~15)
 #endif
@@ -1403,12 +1406,21 @@ __device__ __forceinline__ void long_chunks_loop(const uint32_t* lds, uint32_t l
     auto clampi = [&](uint64_t j) { return j < n ? j : n - 1; };
     // a hole (len == 0) or a missing next chunk prefetches the current chunk's own blocks
     auto pf_geo = [&](const ChunkGeo& nx, const ChunkGeo& cur) -> const ChunkGeo& { return nx.len ? nx : cur; };
+#if BKD_HOLD_LONGLOOP > 0
+    // partials by list position, held (a final chunk's or a hole's word lands in its own unused slot)
+    HeldResults<G, BKD_HOLD_LONGLOOP> held;
+    auto emit = [&](const ChunkGeo& c, uint32_t v) {
+        held.put(v, g, partials, gid, ngroups, n);
+        if (g == 0 && c.len && (c.dst & kPlanFinal)) out[c.dst & ~kPlanFinal] = ~v;
+    };
+#else
     auto emit = [&](const ChunkGeo& c, uint32_t v) {
         if (g == 0 && c.len) {
             if (c.dst & kPlanFinal) out[c.dst & ~kPlanFinal] = ~v;
             else partials[c.dst] = v;
         }
     };
+#endif
 
     u32x4 W0x, Ax[PF], Bx[PF], W0y, Ay[PF], By[PF];
     uint64_t i = gid;
@@ -1419,8 +1431,9 @@ __device__ __forceinline__ void long_chunks_loop(const uint32_t* lds, uint32_t l
     // load), and enough loads issued between a descriptor and its use that the compiler's count of
     // them never reaches back into the current chunk's prefetch.
     PlanDesc dA = descs[clampi(i + ngroups)], dB = descs[clampi(i + 2 * ngroups)];
-    ChunkGeo safe = cur;
-    if (!cur.len) safe.la0 = safe.a = 0, safe.J = 1;  // hole first: prefetch base[0..16)
+    // a hole's prefetch reads base[0, 16) (only plans that overflowed their capacity have holes)
+    ChunkGeo safe;
+    safe.la0 = safe.a = 0, safe.J = 1;
     chunk_prefetch<G, PF, NT>(base, cur.len ? cur : safe, W0x, Ax);
 #define BKD_CHUNK_HALF(DN, W0C, AC, BC, W0N, AN)                                                            \
     {                                                                                                      \
@@ -1434,7 +1447,6 @@ __device__ __forceinline__ void long_chunks_loop(const uint32_t* lds, uint32_t l
         emit(cur, v);                                                                                      \
         if (!more) break;                                                                                  \
         i += ngroups;                                                                                      \
-        if (cur.len) safe = cur;                                                                           \
         cur = nx;                                                                                          \
     }
     for (;;) {
@@ -1454,6 +1466,9 @@ __device__ __forceinline__ void long_chunks_loop(const uint32_t* lds, uint32_t l
         BKD_CHUNK_HALF(dB, W0y, Ay, By, W0x, Ax)
 #endif
     }
+#if BKD_HOLD_LONGLOOP > 0
+    held.finish(g, partials, gid, ngroups, n);
+#endif
 #undef BKD_CHUNK_HALF
 }
 
