@@ -1124,3 +1124,32 @@ def test_resume_longer_than_4gib(gpu):
         h = ck.GpuIntHash(algo)
         assert h.resume(seed, base) == want, algo
         assert h.resume(seed, host) == want, algo  # host buffer > the CPU-route bound: GPU via staging
+
+
+@pytest.mark.parametrize("algo", [ck.CRC32C, ck.CRC32])
+def test_plan_held_partials_past_one_flush(gpu, algo):
+    """The chunk kernel holds each group's partials for 64 rounds of its long loop (HeldResults):
+    1100 entries of 8 MiB + 3 bytes are ~2.25 M full chunks, ~69 rounds per group at 256 CUs, so every
+    group stores one full set of held partials mid-loop and the rest at its end. The plan's digests
+    equal the direct kernel's (one entry per lane group) for every entry and the oracle's on a sample."""
+    import torch
+    n, L = 1100, (8 << 20) + 3
+    total = n * L + 64
+    base = torch.empty(total, dtype=torch.uint8, device=gpu)
+    ck.fill_splitmix64(base, 91)
+    offs = torch.arange(n, dtype=torch.int64, device=gpu) * L + 5
+    lens = torch.full((n,), L, dtype=torch.int32, device=gpu)
+    lens[7] = L - 4096 - 77  # a different head geometry
+    try:
+        ck.set_plan_mode(2)
+        planned = ck.crc_batch(algo, base, offs, lens).cpu().numpy().view(np.uint32)
+        ck.set_plan_mode(1)
+        direct = ck.crc_batch(algo, base, offs, lens).cpu().numpy().view(np.uint32)
+    finally:
+        ck.set_plan_mode(0)
+    assert (planned == direct).all(), np.nonzero(planned != direct)[0][:5]
+    o_np, l_np = offs.cpu().numpy(), lens.cpu().numpy()
+    for i in (0, 7, 549, n - 1):
+        data = base[o_np[i]:o_np[i] + l_np[i]].cpu().numpy()
+        assert planned[i] == oracle.resume(algo, 0, data), i
+    del base
