@@ -733,6 +733,38 @@ __device__ __forceinline__ void held_store_loop(const uint32_t* lds, uint32_t la
     held.finish(g, src.out, gid, ngroups, n);
 }
 
+// Every work item of `src` written (no item left to another launch: PlanDirectSrc with `all`), results
+// held (HeldResults): out-of-range items 0 (and the bounds flag), items under 16 bytes serially.
+#ifndef BKD_HOLD_DIRECT
+#define BKD_HOLD_DIRECT 4  // the chunk kernel's near-uniform direct loop (32 rounds per flush)
+#endif
+template <int G, int PF, bool NT, int K, class Src>
+__device__ __forceinline__ void held_direct_loop(const uint32_t* lds, uint32_t lanereg, int g,
+                                                 const uint8_t* __restrict__ base, const Src& src, uint64_t n,
+                                                 uint64_t gid, uint64_t ngroups, uint32_t* __restrict__ err) {
+    using Gm = Geo<G>;
+    HeldResults<G, K> held;
+    for (uint64_t i = gid; i < n; i += ngroups) {
+        Work wk;
+        const int st = src.get(i, wk);
+        uint32_t v = 0u;
+        if (st == 2) {
+            if (g == 0 && err) atomicOr(err, 1u);
+        } else if (wk.len < 16u) {  // tiny range: serial byte loop (ReflectedIntCrc.java:44-48 form)
+            uint32_t r = wk.r0;
+            const uint8_t* q = base + wk.s;
+            for (uint32_t k = 0; k < wk.len; ++k)
+                r = lds_word(lds, Gm::kByteTabOff + (((r ^ q[k]) & 0xffu) << 2)) ^ (r >> 8);
+            v = r ^ wk.xorout;
+        } else {
+            v = fold_range<G, PF, NT, false, BKD_TAIL_UNCOND != 0, false>(lds, lanereg, g, base, wk.s,
+                                                                         wk.s + (int64_t)wk.len, wk.r0) ^ wk.xorout;
+        }
+        held.put(v, g, src.out, gid, ngroups, n);
+    }
+    held.finish(g, src.out, gid, ngroups, n);
+}
+
 // Uniform batches of short entries (16 B <= len <= 16*G*(PF+1), every load of an entry fits one
 // register set): a group's next entry is loaded while the current one folds (X/Y register sets),
 // so a wave no longer waits one HBM round trip per entry — the one-entry-per-group loop is
@@ -1527,6 +1559,12 @@ __global__ void __launch_bounds__(kBlock) crc_plan_chunks_kernel(const uint8_t* 
     // count[1]: the list position of the first chunk of at most PF + 1 steps (plan_emit_kernel)
     const uint64_t nmain = n ? std::min<uint64_t>(n, count[1]) : 0u;
     if (gid < n) plan_chunks_loop<G, PF, NT>(lds, lanereg, g, base, descs, n, nmain, gid, ngroups, out, partials);
+#if BKD_HOLD_DIRECT > 0
+    // near-uniform batches (every entry here, one per group): results held as the uniform kernel's
+    if (nov && ov.all) {
+        if (gid < nov) held_direct_loop<G, PF, NT, BKD_HOLD_DIRECT>(lds, lanereg, g, base, ov, nov, gid, ngroups, err);
+    } else
+#endif
     if (nov) groups_loop<G, PF, NT>(lds, lanereg, g, base, ov, nov, gid, ngroups, err);
 }
 
