@@ -1663,6 +1663,31 @@ __global__ void __launch_bounds__(256) package_frame_kernel(int64_t ledger_id, c
                                                             uint8_t* __restrict__ frames, uint64_t frame_stride,
                                                             uint32_t mac) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // packed frames (stride 32 + mac, the DigestManager layout package_batch returns) on a 4-byte
+    // boundary: the block's frames are built in LDS and written as consecutive dwords, every store
+    // instruction one contiguous run (a frame per thread wrote 9-10 dwords 36-40 bytes apart)
+    if (frame_stride == 32u + mac && (((uintptr_t)frames) & 3u) == 0) {
+        __shared__ uint32_t fr[256 * 10];
+        const uint32_t fw = (32u + mac) / 4u;  // dwords per frame
+        const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x;
+        const uint32_t cnt = (uint32_t)(n - i0 < (uint64_t)blockDim.x ? n - i0 : (uint64_t)blockDim.x);
+        if (i < n) {
+            const uint64_t fld[4] = {(uint64_t)ledger_id, (uint64_t)entry_ids[i], (uint64_t)lacs[i],
+                                     (uint64_t)length_fields[i]};
+            uint32_t* w = fr + threadIdx.x * fw;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                w[2 * k] = __builtin_bswap32((uint32_t)(fld[k] >> 32));
+                w[2 * k + 1] = __builtin_bswap32((uint32_t)fld[k]);
+            }
+            if (mac == 8u) w[8] = 0u;
+            w[fw - 1u] = __builtin_bswap32(digests[i]);
+        }
+        __syncthreads();
+        uint32_t* dst = reinterpret_cast<uint32_t*>(frames + i0 * frame_stride);
+        for (uint32_t k = threadIdx.x; k < cnt * fw; k += blockDim.x) dst[k] = fr[k];
+        return;
+    }
     if (i >= n) return;
     const uint64_t fld[4] = {(uint64_t)ledger_id, (uint64_t)entry_ids[i], (uint64_t)lacs[i], (uint64_t)length_fields[i]};
     const uint32_t dg = digests[i];
