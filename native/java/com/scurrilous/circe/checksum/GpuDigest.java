@@ -86,5 +86,13 @@ public final class GpuDigest {
                                           long payloadAddrs, long payloadLens, long n, long framesOut,
                                           long frameStride, long digestsOut);
 
+    /** LedgerFragmentReplicator's batch (GpuBatchPackager): the same as packageBatch for n heap payloads
+     *  (the entries' byte[], as Unpooled.wrappedBuffer(data) wraps them) with one lastAddConfirmed for the
+     *  batch; the payloads are copied out with GetByteArrayRegion, never pinned across the call. Returns 0
+     *  or a negative BKD_ERR_* code (a null or short array leaves the JVM's exception pending). */
+    public static native int packageBatchArrays(int algo, long ledgerId, long[] entryIds, long lastAddConfirmed,
+                                                long[] lengthFields, byte[][] payloads, long framesOut,
+                                                long frameStride, long digestsOut);
+
     public static native String lastError();                                       // bkd_last_error
 }

@@ -14,7 +14,8 @@
  *      allocConfig / freeConfig -> bkd_circe_alloc_config / bkd_circe_free_config (same validation)
  * 2. com.scurrilous.circe.checksum.GpuDigest — the batch surface the reference lacks
  *    (INTEGRATION.md §2): device count/init, per-call resume for CRC32C and CRC32, host-memory
- *    batches, and the host-resident DigestManager verify/package batches.
+ *    batches, and the host-resident DigestManager verify/package batches (direct-buffer addresses, or
+ *    the entries' heap arrays for LedgerFragmentReplicator's batch: packageBatchArrays).
  *
  * Built into a loadable library only where a JDK is present (native/jni/Makefile; this image has
  * none). The CPU suite compiles this file with -Wall -Werror against a test-only <jni.h>
@@ -193,6 +194,74 @@ JNIEXPORT jint JNICALL Java_com_scurrilous_circe_checksum_GpuDigest_packageBatch
                                          (const uint32_t*)(intptr_t)payloadLens, (uint64_t)n,
                                          (void*)(intptr_t)framesOut, (uint64_t)frameStride,
                                          (uint32_t*)(intptr_t)digestsOut);
+}
+
+/* LedgerFragmentReplicator's batch of heap payloads (GpuBatchPackager; LedgerFragmentReplicator.java:497-511
+ * wraps each entry's byte[] in Unpooled.wrappedBuffer). The payloads are copied out back to back into one
+ * host buffer (GetByteArrayRegion: no array is pinned across the library call, whose GPU route is a PCIe
+ * round trip) and packaged by bkd_digest_package_batch_host with one lastAddConfirmed for the batch.
+ * Mismatched array lengths leave IllegalArgumentException pending, a null payload NullPointerException. */
+JNIEXPORT jint JNICALL Java_com_scurrilous_circe_checksum_GpuDigest_packageBatchArrays(
+    JNIEnv* env, jclass cls, jint algo, jlong ledgerId, jlongArray entryIds, jlong lastAddConfirmed,
+    jlongArray lengthFields, jobjectArray payloads, jlong framesOut, jlong frameStride, jlong digestsOut) {
+    (void)cls;
+    if (!entryIds || !lengthFields || !payloads) {
+        (*env)->ThrowNew(env, (*env)->FindClass(env, "java/lang/NullPointerException"), "packageBatchArrays");
+        return BKD_ERR_INVALID_ARG;
+    }
+    const jsize n = (*env)->GetArrayLength(env, payloads);
+    if ((*env)->GetArrayLength(env, entryIds) != n || (*env)->GetArrayLength(env, lengthFields) != n) {
+        (*env)->ThrowNew(env, (*env)->FindClass(env, "java/lang/IllegalArgumentException"),
+                         "entryIds, lengthFields and payloads differ in length");
+        return BKD_ERR_INVALID_ARG;
+    }
+    if (n == 0) return BKD_OK;
+    int rc = BKD_ERR_NOMEM;
+    uint64_t total = 0;
+    int64_t* ids = (int64_t*)malloc((size_t)n * sizeof(int64_t));
+    int64_t* lacs = (int64_t*)malloc((size_t)n * sizeof(int64_t));
+    int64_t* lfs = (int64_t*)malloc((size_t)n * sizeof(int64_t));
+    const void** ptrs = (const void**)malloc((size_t)n * sizeof(void*));
+    uint32_t* lens = (uint32_t*)malloc((size_t)n * sizeof(uint32_t));
+    char* staging = NULL;
+    if (!ids || !lacs || !lfs || !ptrs || !lens) goto done;
+    (*env)->GetLongArrayRegion(env, entryIds, 0, n, (jlong*)ids);
+    (*env)->GetLongArrayRegion(env, lengthFields, 0, n, (jlong*)lfs);
+    for (jsize i = 0; i < n; ++i) {  /* pass 1: the payload lengths */
+        lacs[i] = lastAddConfirmed;
+        jbyteArray a = (jbyteArray)(*env)->GetObjectArrayElement(env, payloads, i);
+        if (!a) {
+            (*env)->ThrowNew(env, (*env)->FindClass(env, "java/lang/NullPointerException"), "null payload");
+            rc = BKD_ERR_INVALID_ARG;
+            goto done;
+        }
+        lens[i] = (uint32_t)(*env)->GetArrayLength(env, a);
+        total += lens[i];
+        (*env)->DeleteLocalRef(env, a);
+    }
+    staging = (char*)malloc(total ? (size_t)total : 1u);
+    if (!staging) goto done;
+    total = 0;
+    for (jsize i = 0; i < n; ++i) {  /* pass 2: the bytes, back to back */
+        jbyteArray a = (jbyteArray)(*env)->GetObjectArrayElement(env, payloads, i);
+        (*env)->GetByteArrayRegion(env, a, 0, (jsize)lens[i], (jbyte*)(staging + total));
+        (*env)->DeleteLocalRef(env, a);
+        ptrs[i] = staging + total;
+        total += lens[i];
+    }
+    rc = (*env)->ExceptionCheck(env)
+             ? BKD_ERR_INVALID_ARG
+             : bkd_digest_package_batch_host(algo, ledgerId, ids, lacs, lfs, (const void* const*)ptrs, lens,
+                                             (uint64_t)n, (void*)(intptr_t)framesOut, (uint64_t)frameStride,
+                                             (uint32_t*)(intptr_t)digestsOut);
+done:
+    free(staging);
+    free(lens);
+    free((void*)ptrs);
+    free(lfs);
+    free(lacs);
+    free(ids);
+    return rc;
 }
 
 JNIEXPORT jstring JNICALL Java_com_scurrilous_circe_checksum_GpuDigest_lastError(JNIEnv* env, jclass cls) {

@@ -11,7 +11,7 @@
 
 #include "jni.h"
 
-enum { K_BYTES = 1, K_INTS, K_DIRECT, K_STRING, K_CLASS };
+enum { K_BYTES = 1, K_INTS, K_DIRECT, K_STRING, K_CLASS, K_LONGS, K_OBJECTS };
 
 struct _jobject {
     int kind;
@@ -103,9 +103,35 @@ static jstring j_new_string_utf(JNIEnv* env, const char* s) {
     return new_obj(K_STRING, s, strlen(s) + 1, (jsize)strlen(s));
 }
 
+static jobject j_get_object_array_element(JNIEnv* env, jobjectArray a, jsize i) {
+    (void)env;
+    if (i < 0 || i >= a->len) {
+        set_pending("java/lang/ArrayIndexOutOfBoundsException", "element");
+        return NULL;
+    }
+    return ((jobject*)a->data)[i];
+}
+
+static void j_get_long_array_region(JNIEnv* env, jlongArray a, jsize start, jsize len, jlong* buf) {
+    (void)env;
+    if (start < 0 || len < 0 || (int64_t)start + len > (int64_t)a->len) {
+        set_pending("java/lang/ArrayIndexOutOfBoundsException", "region");
+        return;
+    }
+    memcpy(buf, (const jlong*)a->data + start, (size_t)len * sizeof(jlong));
+}
+
+static int g_local_refs_deleted;
+static void j_delete_local_ref(JNIEnv* env, jobject o) {
+    (void)env;
+    (void)o;
+    ++g_local_refs_deleted;  /* the objects stay owned by the test */
+}
+
 static const struct JNINativeInterface_ g_table = {
     j_find_class,   j_throw_new,        j_exception_check, j_get_array_length, j_get_byte_array_region,
-    j_get_critical, j_release_critical, j_direct_address,  j_new_string_utf,
+    j_get_critical, j_release_critical, j_direct_address,  j_new_string_utf,   j_get_object_array_element,
+    j_get_long_array_region, j_delete_local_ref,
 };
 static JNIEnv g_env = &g_table;
 
@@ -115,6 +141,14 @@ JNIEXPORT jobject fake_byte_array(const void* data, jsize len) { return new_obj(
 JNIEXPORT jobject fake_int_array(const int32_t* data, jsize len) {
     return new_obj(K_INTS, data, (size_t)len * sizeof(int32_t), len);
 }
+JNIEXPORT jobject fake_long_array(const int64_t* data, jsize len) {
+    return new_obj(K_LONGS, data, (size_t)len * sizeof(int64_t), len);
+}
+/* a byte[][]: the element objects stay owned by the caller (fake_free frees only the array itself) */
+JNIEXPORT jobject fake_object_array(const jobject* elems, jsize len) {
+    return new_obj(K_OBJECTS, elems, (size_t)len * sizeof(jobject), len);
+}
+JNIEXPORT int fake_local_refs_deleted(void) { return g_local_refs_deleted; }
 JNIEXPORT jobject fake_direct_buffer(void* addr) { return new_obj(K_DIRECT, addr, 0, 0); }
 JNIEXPORT const char* fake_string(jobject s) { return s && s->kind == K_STRING ? (const char*)s->data : NULL; }
 JNIEXPORT void fake_free(jobject o) {

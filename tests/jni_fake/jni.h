@@ -31,6 +31,8 @@ typedef jobject jthrowable;
 typedef jobject jarray;
 typedef jarray jbyteArray;
 typedef jarray jintArray;
+typedef jarray jlongArray;
+typedef jarray jobjectArray;
 
 struct JNINativeInterface_;
 typedef const struct JNINativeInterface_* JNIEnv;
@@ -46,6 +48,9 @@ struct JNINativeInterface_ {
     void (*ReleasePrimitiveArrayCritical)(JNIEnv* env, jarray array, void* carray, jint mode);
     void* (*GetDirectBufferAddress)(JNIEnv* env, jobject buf);
     jstring (*NewStringUTF)(JNIEnv* env, const char* utf);
+    jobject (*GetObjectArrayElement)(JNIEnv* env, jobjectArray array, jsize index);
+    void (*GetLongArrayRegion)(JNIEnv* env, jlongArray array, jsize start, jsize len, jlong* buf);
+    void (*DeleteLocalRef)(JNIEnv* env, jobject ref);
 };
 
 #endif

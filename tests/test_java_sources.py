@@ -114,6 +114,23 @@ MEMBERS = [
     ("org.apache.bookkeeper.util.ByteBufList", r"public ByteBuf getBuffer\(int index\)"),
     ("org.apache.bookkeeper.util.ByteBufList", r"public int size\(\)"),
     ("org.apache.bookkeeper.client.BatchedReadOp", r"lh\.macManager\.verifyDigestAndReturnData\(eId \+ i, buffer\)"),
+    # GpuBatchPackager
+    ("org.apache.bookkeeper.proto.checksum.DigestManager", r"\n    final boolean useV2Protocol;"),
+    ("org.apache.bookkeeper.proto.checksum.DigestManager", r"\n    final int macCodeLength;"),
+    ("org.apache.bookkeeper.proto.checksum.DigestManager",
+     r"public ReferenceCounted computeDigestAndPackageForSending\(long entryId, long lastAddConfirmed, long length,\s+"
+     r"ByteBuf data, byte\[\] masterKey, int flags\)"),
+    ("org.apache.bookkeeper.proto.BookieProtoEncoding", r"public static final int SMALL_ENTRY_SIZE_THRESHOLD = 16 \* 1024;"),
+    ("org.apache.bookkeeper.proto.BookieProtocol", r"public static int toInt\(byte version, byte opCode, short flags\)"),
+    ("org.apache.bookkeeper.proto.BookieProtocol", r"byte CURRENT_PROTOCOL_VERSION = 2;"),
+    ("org.apache.bookkeeper.proto.BookieProtocol", r"byte ADDENTRY = 1;"),
+    ("org.apache.bookkeeper.proto.BookieProtocol", r"int MASTER_KEY_LENGTH = 20;"),
+    ("org.apache.bookkeeper.util.ByteBufList", r"public static ByteBufList get\(ByteBuf b1, ByteBuf b2\)"),
+    ("org.apache.bookkeeper.client.LedgerHandle", r"\n    final ClientContext clientCtx;"),
+    ("org.apache.bookkeeper.client.ClientContext", r"ByteBufAllocator getByteBufAllocator\(\);"),
+    ("org.apache.bookkeeper.client.LedgerFragmentReplicator",
+     r"computeDigestAndPackageForSending\(entry\.getEntryId\(\),\s+lh\.getLastAddConfirmed\(\), entry\.getLength\(\),\s+"
+     r"Unpooled\.wrappedBuffer\(data, 0, data\.length\),"),
 ]
 
 
@@ -131,3 +148,115 @@ def test_integration_doc_names_the_loaded_library():
     assert 'loadLibraryFromJar("/lib/libcirce-checksum." + NativeUtils.libType())' in gd
     assert "libbkdigest-jni" not in doc
     assert "GpuProviderChain.select()" in doc and "GpuBatchVerifier.verifiedPrefix" in doc
+
+
+# ---- GpuBatchVerifier leaves the buffers as verifyDigestAndReturnData does ----
+VERIFIER = os.path.join(JAVA, "org", "apache", "bookkeeper", "proto", "checksum", "GpuBatchVerifier.java")
+READER_INDEX_SET = "bufList.getBuffer(i).readerIndex(DigestManager.METADATA_LENGTH + dm.macCodeLength);"
+
+
+def _method_body(src, signature):
+    """The text between the braces of the method whose declaration contains `signature`, comments removed."""
+    src = re.sub(r"/\*.*?\*/|//[^\n]*", "", src, flags=re.S)
+    start = src.index(signature)
+    k = src.index("{", start)
+    depth = 0
+    for j in range(k, len(src)):
+        depth += {"{": 1, "}": -1}.get(src[j], 0)
+        if depth == 0:
+            return src[k + 1:j]
+    raise AssertionError("unbalanced braces")
+
+
+def verifier_problems(src):
+    """Why the batched verify hook would leave buffers (or CRC bytes) unlike the reference's loop
+    (BatchedReadOp.java:175-189 -> DigestManager.verifyDigestAndReturnData, DigestManager.java:333-338);
+    an empty list when it does not. Source-text checks (no JDK here)."""
+    problems = []
+    body = _method_body(src, "public static int verifiedPrefix(")
+    flat = re.sub(r"\s+", " ", body)
+    # 1. the GPU route only for buffers nothing has been read from: the reference CRCs absolute
+    #    offsets of memoryAddress() (DigestManager.java:62-64,236-239) and reads ids at readerIndex
+    if not re.search(r"direct = [^;]*\.hasMemoryAddress\(\) && \w+\.readerIndex\(\) == 0;", flat):
+        problems.append("no readerIndex() == 0 guard on the GPU route")
+    if re.search(r"memoryAddress\(\) \+ \w+\.readerIndex\(\)", flat):
+        problems.append("frame address offset by readerIndex (the reference addresses absolute offsets)")
+    call = flat.find("GpuDigest.verifyBatch(")
+    if call < 0:
+        return problems + ["no GpuDigest.verifyBatch call"]
+    after = flat[call:]
+    # 2. every exit after the library call: the untouched fallback (rc < 0), or the verified count
+    #    after the readerIndex loop over exactly the verified prefix (DigestManager.java:336)
+    loop = re.search(r"for \(int i = 0; i < verified; i\+\+\) \{ " + re.escape(READER_INDEX_SET) + r" \}", after)
+    for m in re.finditer(r"return ([^;]*);", after):
+        ret = m.group(1).strip()
+        if ret == "serialPrefix(dm, firstEntryId, bufList)":
+            if not re.search(r"if \(rc < 0\) \{ $", after[:m.start()]):
+                problems.append("a serial fallback after the library call not guarded by rc < 0")
+            if loop and m.start() > loop.start():
+                problems.append("a serial fallback after buffers were already advanced")
+        elif ret == "verified":
+            if not loop or loop.end() > m.start():
+                problems.append("the verified count is returned without the readerIndex loop before it")
+        else:
+            problems.append(f"an exit that skips the readerIndex loop: return {ret};")
+    if not re.search(r"final int verified = \(int\) rc;", after):
+        problems.append("verified is not the library's verified prefix")
+    return problems
+
+
+def test_batch_verifier_leaves_buffers_as_the_reference():
+    assert verifier_problems(open(VERIFIER).read()) == []
+    # the reference member the loop relies on (package-private, same package)
+    dm = open(_ref_class_file("org.apache.bookkeeper.proto.checksum.DigestManager")).read()
+    assert re.search(r"\n    final int macCodeLength;", dm)
+    assert "dataReceived.readerIndex(METADATA_LENGTH + macCodeLength);" in dm  # DigestManager.java:336
+
+
+@pytest.mark.parametrize("mutation", [
+    ("bufList.getBuffer(i).readerIndex(DigestManager.METADATA_LENGTH + dm.macCodeLength);", ""),  # round-5 code
+    ("&& b.readerIndex() == 0", ""),
+    ("addrs.writeLongLE(b.memoryAddress());", "addrs.writeLongLE(b.memoryAddress() + b.readerIndex());"),
+    ("return verified;", "return (int) rc;"),
+    ("i < verified; i++", "i < n; i++"),
+])
+def test_batch_verifier_check_catches(mutation):
+    """The check above fails on each way the hook can diverge (the round-5 hook had the first and third)."""
+    src = open(VERIFIER).read()
+    old, new = mutation
+    assert old in src
+    assert verifier_problems(src.replace(old, new)) != []
+
+
+def test_batch_packager_builds_the_reference_objects():
+    """GpuBatchPackager's V2 buffer is built with the statements of computeDigestAndPackageForSendingV2
+    (DigestManager.java:126-167) — the same small-entry test, header sizes, allocation, the three
+    leading writes and the small/large tail — with the 32-byte header and digest (there
+    writeLong x 4 + populateValueAndReset) taken from the library's frame; V3 is
+    ByteBufList.get(header buffer of METADATA_LENGTH + macCodeLength, data) (:169-181)."""
+    ref = re.sub(r"\s+", " ", _method_body(open(_ref_class_file("org.apache.bookkeeper.proto.checksum.DigestManager")).read(),
+                                          "private ReferenceCounted computeDigestAndPackageForSendingV2("))
+    src = open(os.path.join(JAVA, "org", "apache", "bookkeeper", "proto", "checksum", "GpuBatchPackager.java")).read()
+    ours = re.sub(r"\s+", " ", _method_body(src, "private static ReferenceCounted packageV2("))
+    for stmt in ["boolean isSmallEntry = data.readableBytes() < BookieProtoEncoding.SMALL_ENTRY_SIZE_THRESHOLD;",
+                 "int payloadSize = data.readableBytes();",
+                 "int bufferSize = 4 + headersSize + (isSmallEntry ? payloadSize : 0);",
+                 "ByteBuf buf = allocator.buffer(bufferSize, bufferSize);",
+                 "buf.writeInt(headersSize + payloadSize);",
+                 "buf.writeBytes(masterKey, 0, BookieProtocol.MASTER_KEY_LENGTH);",
+                 "buf.writeBytes(data, data.readerIndex(), data.readableBytes()); data.release(); return buf; }",
+                 "return ByteBufList.get(buf, data);"]:
+        assert stmt in ref, stmt
+        assert stmt in ours, stmt
+    toint = "BookieProtocol.PacketHeader.toInt( BookieProtocol.CURRENT_PROTOCOL_VERSION, BookieProtocol.ADDENTRY, (short) flags));"
+    assert toint in ref and toint in ours
+    # headersSize: 4 + master key + METADATA_LENGTH + macCodeLength (frameLen = METADATA_LENGTH + macCodeLength)
+    assert "int headersSize = 4 + BookieProtocol.MASTER_KEY_LENGTH + METADATA_LENGTH + macCodeLength;" in ref
+    assert "int headersSize = 4 + BookieProtocol.MASTER_KEY_LENGTH + frameLen;" in ours
+    body = re.sub(r"\s+", " ", _method_body(src, "public static ReferenceCounted[] packageEntries("))
+    assert "final int frameLen = DigestManager.METADATA_LENGTH + dm.macCodeLength;" in body
+    assert "ByteBufList.get(Unpooled.buffer(frameLen).writeBytes(frames, i * frameLen, frameLen), data)" in body
+    assert "Unpooled.wrappedBuffer(payloads[i], 0, payloads[i].length)" in body  # LedgerFragmentReplicator.java:509
+    # the header + digest bytes written in place of writeLong x 4 + populateValueAndReset come after the master key
+    assert ours.index("buf.writeBytes(masterKey") < ours.index("buf.writeBytes(frames, at, frameLen);") < ours.index(
+        "if (isSmallEntry)")

@@ -15,7 +15,8 @@ declarations (Sse42Crc32C.java:119-129):
   * allocConfig's validation matrix (:56-62): empty, first < min_words, non-decreasing, below
     min_words; a valid ladder returns a handle that freeConfig releases;
   * the GpuDigest batch class: resumeAddress for both polynomials, resumeBatch, verifyBatch's
-    verified prefix and its error return, packageBatch's frames, lastError.
+    verified prefix and its error return, packageBatch's frames, packageBatchArrays over heap
+    payloads (GpuBatchPackager, LedgerFragmentReplicator's batch) with its argument errors, lastError.
 """
 import ctypes
 import os
@@ -64,7 +65,8 @@ def shim(tmp_path_factory):
         "fake_direct_buffer": (vp, [vp]), "fake_string": (ctypes.c_char_p, [vp]), "fake_free": (None, [vp]),
         "fake_pending": (ctypes.c_char_p, []), "fake_clear": (None, []), "fake_critical_depth": (i32, []),
         "fake_critical_total": (i32, []), "fake_fail_critical": (None, [i32]), "fake_fail_malloc": (None, [i32]),
-        "fake_malloc_calls": (i32, []),
+        "fake_malloc_calls": (i32, []), "fake_long_array": (vp, [vp, i32]), "fake_object_array": (vp, [vp, i32]),
+        "fake_local_refs_deleted": (i32, []),
         SSE + "nativeSupported": (ctypes.c_uint8, [vp, vp]),
         SSE + "nativeArray": (i32, [vp, vp, i32, vp, i32, i32, i64]),
         SSE + "nativeDirectBuffer": (i32, [vp, vp, i32, vp, i32, i32, i64]),
@@ -78,6 +80,7 @@ def shim(tmp_path_factory):
         GPU + "resumeBatch": (i32, [vp, vp, i32, i64, i64, i64, i64, i64, i64, i32, i64]),
         GPU + "verifyBatch": (i64, [vp, vp, i32, i64, i64, ctypes.c_uint8, i64, i64, i64, i64]),
         GPU + "packageBatch": (i32, [vp, vp, i32, i64, i64, i64, i64, i64, i64, i64, i64, i64, i64]),
+        GPU + "packageBatchArrays": (i32, [vp, vp, i32, i64, vp, i64, vp, vp, i64, i64, i64]),
         GPU + "lastError": (vp, [vp, vp]),
     }
     for name, (res, args) in sig.items():
@@ -307,3 +310,66 @@ def test_gpu_digest_package_batch(shim, env):
             d, hdr = oracle.digest_entry(algo, 9, int(ids[i]), int(lacs[i]), int(lfs[i]), payloads[i])
             assert digests[i] == d
             assert frames[i * stride:i * stride + 32 + mac].tobytes() == hdr + oracle.digest_bytes(algo, d)
+
+
+def _long_array(S, values):
+    a = np.ascontiguousarray(values, dtype=np.int64)
+    return S.fake_long_array(a.ctypes.data, a.size)
+
+
+@pytest.mark.parametrize("algo", [CRC32C, CRC32])
+def test_gpu_digest_package_batch_arrays(shim, env, algo):
+    """GpuDigest.packageBatchArrays: LedgerFragmentReplicator's batch of heap byte[] payloads
+    (LedgerFragmentReplicator.java:497-511) -> frame i = the 32-byte BE header [ledger, entry, LAC,
+    length] + the digest, as computeDigestAndPackageForSending writes them (DigestManager.java:146-153,
+    172-177), and digest i; lengths 0, 1, odd, 16 KiB +/- 1 (the V2 small-entry bound), 70 000."""
+    rng = np.random.default_rng(31 + algo)
+    mac = 4 if algo == CRC32C else 8
+    sizes = [0, 1, 7, 4096, 16383, 16384, 16385, 70000] + [int(v) for v in rng.integers(0, 9000, 40)]
+    n = len(sizes)
+    payloads = [rng.bytes(k) for k in sizes]
+    arrays = [_barray(shim, p) for p in payloads]
+    objs = (ctypes.c_void_p * n)(*arrays)
+    parr = shim.fake_object_array(objs, n)
+    ids = np.arange(500, 500 + n, dtype=np.int64)
+    lfs = np.array([len(p) + 3 for p in payloads], dtype=np.int64)  # length fields need not equal the payload
+    lac = 499
+    frames = np.zeros(n * (32 + mac), dtype=np.uint8)
+    digests = np.zeros(n, dtype=np.uint32)
+    idarr, lfarr = _long_array(shim, ids), _long_array(shim, lfs)
+    f = getattr(shim, GPU + "packageBatchArrays")
+    deleted = shim.fake_local_refs_deleted()
+    rc = f(env, None, algo, 77, idarr, lac, lfarr, parr, frames.ctypes.data, 32 + mac, digests.ctypes.data)
+    assert rc == 0 and shim.fake_pending() == b""
+    assert shim.fake_local_refs_deleted() - deleted == 2 * n  # every element reference released
+    for i, p in enumerate(payloads):
+        d, hdr = oracle.digest_entry(algo, 77, int(ids[i]), lac, int(lfs[i]), p)
+        assert digests[i] == d, i
+        assert frames[i * (32 + mac):(i + 1) * (32 + mac)].tobytes() == hdr + oracle.digest_bytes(algo, d), i
+    # SURVEY §8c framing vectors: ledger 1, entry 1, LAC 0, payload b[i] = (byte) i of 16 383 / 16 384 B
+    want = {CRC32C: (0x24656066, 0x6fa1a26b), CRC32: (0xdf2ebb5b, 0x4512b34e)}[algo]
+    for k, L in enumerate((16383, 16384)):
+        one = _barray(shim, bytes(i & 0xFF for i in range(L)))
+        oa = shim.fake_object_array((ctypes.c_void_p * 1)(one), 1)
+        a1, l1 = _long_array(shim, [1]), _long_array(shim, [L])
+        fr = np.zeros(32 + mac, dtype=np.uint8)
+        dg = np.zeros(1, dtype=np.uint32)
+        assert f(env, None, algo, 1, a1, 0, l1, oa, fr.ctypes.data, 32 + mac, dg.ctypes.data) == 0
+        assert dg[0] == want[k]
+        for o in (one, oa, a1, l1):
+            shim.fake_free(o)
+    # argument errors leave the JVM's exception pending and return a negative code
+    short = _long_array(shim, ids[:-1])
+    assert f(env, None, algo, 77, short, lac, lfarr, parr, frames.ctypes.data, 32 + mac, digests.ctypes.data) < 0
+    assert shim.fake_pending().startswith(b"java/lang/IllegalArgumentException")
+    shim.fake_clear()
+    objs[3] = None
+    holey = shim.fake_object_array(objs, n)
+    assert f(env, None, algo, 77, idarr, lac, lfarr, holey, frames.ctypes.data, 32 + mac, digests.ctypes.data) < 0
+    assert shim.fake_pending().startswith(b"java/lang/NullPointerException")
+    shim.fake_clear()
+    empty = shim.fake_object_array(objs, 0)
+    e0 = _long_array(shim, [])
+    assert f(env, None, algo, 77, e0, lac, e0, empty, frames.ctypes.data, 32 + mac, digests.ctypes.data) == 0
+    for o in arrays + [parr, idarr, lfarr, short, holey, empty, e0]:
+        shim.fake_free(o)

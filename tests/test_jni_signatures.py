@@ -16,7 +16,8 @@ SHIM = os.path.join(ROOT, "native", "jni", "bkdigest_jni.c")
 
 # Java type -> JNI C type (JNI specification, "Primitive Types" / "Reference Types")
 JNI = {"boolean": "jboolean", "int": "jint", "long": "jlong", "void": "void", "byte[]": "jbyteArray",
-       "int[]": "jintArray", "ByteBuffer": "jobject", "String": "jstring"}
+       "int[]": "jintArray", "long[]": "jlongArray", "byte[][]": "jobjectArray", "ByteBuffer": "jobject",
+       "String": "jstring"}
 
 # Sse42Crc32C.java:119-129, verbatim method signatures (return type, name, parameter types)
 SSE42 = [
@@ -36,6 +37,7 @@ GPU_DIGEST = [
     ("int", "resumeBatch", ["int", "long", "long", "long", "long", "long", "long", "int", "long"]),
     ("long", "verifyBatch", ["int", "long", "long", "boolean", "long", "long", "long", "long"]),
     ("int", "packageBatch", ["int", "long", "long", "long", "long", "long", "long", "long", "long", "long", "long"]),
+    ("int", "packageBatchArrays", ["int", "long", "long[]", "long", "long[]", "byte[][]", "long", "long", "long"]),
     ("String", "lastError", []),
 ]
 CLASSES = {"com.scurrilous.circe.crc.Sse42Crc32C": SSE42, "com.scurrilous.circe.checksum.GpuDigest": GPU_DIGEST}
