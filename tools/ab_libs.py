@@ -76,8 +76,10 @@ def main(paths):
     hsep_al_o, hsep_o = sep_base, sep_base + (hs_o % 128)
     m1_l = np.where(np.arange(n) % 256 == 0, 2048, 1024)  # 1 KiB chunks through the plan (outside the gate's band)
     m1_o = np.concatenate([[0], np.cumsum(m1_l[:-1])])
+    order = np.argsort(-lens, kind="stable")  # the same entries, index sorted by descending length
     work = {
         "zipf": (0, *idx(offs, lens), total),
+        "zipf_sorted": (0, *idx(offs[order], lens[order]), total),
         "zipf_crc32": (1, *idx(offs, lens), total),
         "zipf_lt1k": (0, *idx(offs[lt], lens[lt]), int(lens[lt].sum())),
         "zipf_heads": (0, *idx(head_o, head_l), int(head_l.sum())),

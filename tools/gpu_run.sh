@@ -7,6 +7,7 @@
 #   tests            pytest -m gpu (the driver's suite)        tests:EXPR  only tests matching -k EXPR
 #   smoke            __graft_entry__.smoke()
 #   driver           bench.py --gpus 1 --steps 20 --warmup 5 (the driver's command)
+#   trace            the driver's command with --trace-launches (HIP events around every launch)
 #   bench100         bench.py --steps 100 --warmup 50
 #   zipf | zipf32    bench.py --config zipf [--algo crc32]
 #   verify | shard8m bench.py --config verify4k | shard8m
@@ -35,6 +36,7 @@ for step in "$@"; do
     tests:*) run pytest_gpu_sel 900 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests -k "${step#tests:}" ;;
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     driver) run bench_driver 200 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    trace) run bench_driver_trace 200 python3 bench.py --gpus 1 --steps 20 --warmup 5 --trace-launches ;;
     bench100) run bench_100 200 python3 bench.py --steps 100 --warmup 50 --no-cpu-baseline ;;
     zipf) run bench_zipf 300 python3 bench.py --config zipf ;;
     zipf32) run bench_zipf_crc32 300 python3 bench.py --config zipf --algo crc32 ;;
