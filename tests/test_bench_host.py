@@ -29,3 +29,17 @@ def test_zipf_index_matches_survey_shape():
     assert 5000 < lens.mean() < 8000  # mean ~6 484 B on 1M entries
     o2, l2 = bench.zipf_index(1 << 16)
     assert np.array_equal(offs, o2) and np.array_equal(lens, l2)  # seeded
+
+
+def test_only_config2_carries_the_headline_metric():
+    """BASELINE.json's metric names config 2 (1M x 4 KiB, CRC32C) only; every other
+    workload's line names itself (Zipf, CRC32, config 4's shard), so none can be read as the headline."""
+    import json
+    import os
+    base = json.load(open(os.path.join(os.path.dirname(bench.__file__), "BASELINE.json")))
+    assert bench.metric_for("uniform4k", "crc32c") == base["metric"] == bench.METRIC
+    others = [bench.metric_for(c, a) for c in ("uniform4k", "shard8m", "zipf", "indexed4k") for a in ("crc32c", "crc32")
+              if (c, a) != ("uniform4k", "crc32c")]
+    assert len(set(others)) == len(others) and base["metric"] not in others
+    assert "Zipf" in bench.metric_for("zipf", "crc32") and "CRC32 " in bench.metric_for("zipf", "crc32")
+    assert "config 4" in bench.metric_for("shard8m", "crc32c")
