@@ -41,7 +41,14 @@ def main() -> None:
     args = ap.parse_args()
     import torch
     libs = args.libs or [os.path.join(ROOT, "bookkeeper_amd", "libbkdigest.so")]
-    Ls = [(os.path.basename(p), load_lib(p)) for p in libs]
+    # a library may carry ":LANES" (bkd_set_group_lanes before its launches; the same file loads once)
+    loaded = {}
+    Ls = []
+    for spec in libs:
+        path, _, lanes = spec.partition(":")
+        if path not in loaded:
+            loaded[path] = load_lib(path)
+        Ls.append((os.path.basename(path) + (f":{lanes}" if lanes else ""), loaded[path], int(lanes or 0)))
     probe = None
     if args.probe:
         probe = ctypes.CDLL(os.path.join(HERE, "libclockprobe.so"))
@@ -59,7 +66,8 @@ def main() -> None:
     torch.cuda.synchronize()
     ref = None
     for rnd in range(args.rounds):
-        for name, L in Ls:
+        for name, L, lanes in Ls:
+            L.bkd_set_group_lanes(lanes)
             time.sleep(args.idle_ms / 1e3)
             evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                    for _ in range(args.launches)]
