@@ -242,8 +242,12 @@ JNIEXPORT jint JNICALL Java_com_scurrilous_circe_checksum_GpuDigest_packageBatch
     staging = (char*)malloc(total ? (size_t)total : 1u);
     if (!staging) goto done;
     total = 0;
-    for (jsize i = 0; i < n; ++i) {  /* pass 2: the bytes, back to back */
+    for (jsize i = 0; i < n && !(*env)->ExceptionCheck(env); ++i) {  /* pass 2: the bytes, back to back */
         jbyteArray a = (jbyteArray)(*env)->GetObjectArrayElement(env, payloads, i);
+        if (!a) {  /* replaced by null since pass 1 (another thread) */
+            (*env)->ThrowNew(env, (*env)->FindClass(env, "java/lang/NullPointerException"), "null payload");
+            break;
+        }
         (*env)->GetByteArrayRegion(env, a, 0, (jsize)lens[i], (jbyte*)(staging + total));
         (*env)->DeleteLocalRef(env, a);
         ptrs[i] = staging + total;
