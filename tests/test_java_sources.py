@@ -30,10 +30,14 @@ JAVA_LANG = {"String", "Object", "Throwable", "Exception", "RuntimeException", "
              "IndexOutOfBoundsException", "System", "Math", "Integer", "Long", "Override", "Boolean"}
 
 
+JAVA_TEST = os.path.join(ROOT, "native", "java-test")
+
+
 def _sources():
     files = sorted(glob.glob(os.path.join(JAVA, "**", "*.java"), recursive=True))
     assert len(files) >= 4
-    return files
+    # the maintainer-run JUnit test of the batch hooks (native/java-test), resolved the same way
+    return files + sorted(glob.glob(os.path.join(JAVA_TEST, "**", "*.java"), recursive=True))
 
 
 def _package(src):
@@ -69,7 +73,7 @@ def test_imports_resolve(path):
     assert path.endswith(os.path.join(*pkg.split("."), os.path.basename(path))), "file sits in its package dir"
     imported = set()
     for static, name in re.findall(r"^import\s+(static\s+)?([\w.]+);", src, re.M):
-        if name.startswith(("java.", "javax.", "io.netty.")):
+        if name.startswith(("java.", "javax.", "io.netty.", "org.junit.")):
             imported.add(name.rsplit(".", 1)[1])
             continue
         fq = name.rsplit(".", 1)[0] if static else name
@@ -127,6 +131,15 @@ MEMBERS = [
     ("org.apache.bookkeeper.proto.BookieProtocol", r"int MASTER_KEY_LENGTH = 20;"),
     ("org.apache.bookkeeper.util.ByteBufList", r"public static ByteBufList get\(ByteBuf b1, ByteBuf b2\)"),
     ("org.apache.bookkeeper.client.LedgerHandle", r"\n    final ClientContext clientCtx;"),
+    # native/java-test/.../GpuBatchHooksTest.java
+    ("org.apache.bookkeeper.util.ByteBufList", r"public byte\[\] toArray\(\)"),
+    ("org.apache.bookkeeper.util.ByteBufList", r"public static ByteBufList get\(\)"),
+    ("org.apache.bookkeeper.util.ByteBufList", r"public void add\(ByteBuf buf\)"),
+    ("org.apache.bookkeeper.proto.BookieProtocol", r"short FLAG_RECOVERY_ADD = 0x0002;"),
+    ("org.apache.bookkeeper.proto.checksum.CRC32CDigestManager",
+     r"public CRC32CDigestManager\(long ledgerId, boolean useV2Protocol, ByteBufAllocator allocator\)"),
+    ("org.apache.bookkeeper.proto.checksum.CRC32DigestManager",
+     r"public CRC32DigestManager\(long ledgerId, boolean useV2Protocol, ByteBufAllocator allocator\)"),
     ("org.apache.bookkeeper.client.ClientContext", r"ByteBufAllocator getByteBufAllocator\(\);"),
     ("org.apache.bookkeeper.client.LedgerFragmentReplicator",
      r"computeDigestAndPackageForSending\(entry\.getEntryId\(\),\s+lh\.getLastAddConfirmed\(\), entry\.getLength\(\),\s+"
