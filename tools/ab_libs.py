@@ -4,7 +4,7 @@ effects being measured).
 
 Usage (GPU box): python3 tools/ab_libs.py [lib.so ...]
 Default libraries: bookkeeper_amd/libbkdigest.so and every tools/variants/lib_*.so.
-Workloads: zipf (config 3), zipf crc32, zipf < 1 KiB bucket, packed 64 B, indexed 4 KiB, uniform 4 KiB.
+Workloads: zipf (config 3), zipf crc32, zipf < 1 KiB bucket, zipf's full chunks / heads alone, packed 64 B, indexed 4 KiB, uniform 4 KiB.
 Each library's digests must equal the first library's, bit for bit.
 Environment: AB_WORK (workload names), AB_ROUNDS, AB_MODE (plan mode), AB_SMALL / AB_SHORT_MEAN
 (short-entry class bound and gate), AB_LANES (direct-kernel lanes), AB_PF (chunk-kernel loads in
@@ -77,11 +77,34 @@ def main(paths):
     m1_l = np.where(np.arange(n) % 256 == 0, 2048, 1024)  # 1 KiB chunks through the plan (outside the gate's band)
     m1_o = np.concatenate([[0], np.cumsum(m1_l[:-1])])
     order = np.argsort(-lens, kind="stable")  # the same entries, index sorted by descending length
+    # config 3 split as the plan splits it (CH = 4 KiB, chunks ending on ae = the entry's end rounded
+    # up to 128 B, a head shorter than 16 B merged): the full chunks alone as aligned 4 KiB entries at
+    # their own addresses, in the plan's list order (entry order, chunk 0 = the entry's last) or by
+    # address; and the heads alone at their own addresses (an entry's head ends on its first full chunk)
+    z_ae = (offs + lens + 127) // 128 * 128
+    z_m = (z_ae - offs + 4095) // 4096
+    z_hl = z_ae - offs - (z_m - 1) * 4096
+    z_mg = (z_hl < 16) & (z_m > 1)
+    z_m = np.where(z_mg, z_m - 1, z_m)
+    z_hl = np.where(z_mg, z_hl + 4096, z_hl)
+    z_fullh = (z_hl + 127) // 128 == 32  # a head of exactly 32 steps sits in the full bin
+    z_full = (z_m - 1) + z_fullh
+    z_own = np.repeat(np.arange(n), z_full)
+    z_c = np.arange(z_own.size) - np.repeat(np.cumsum(z_full) - z_full, z_full)
+    zf_o = z_ae[z_own] - (z_c + 1) * 4096
+    zf_l = np.full(zf_o.size, 4096)
+    zf_l[5] = 2048  # out of the near-uniform gate's band, as plan4k
+    zh_sel = ~z_fullh
+    zh_o = offs[zh_sel]
+    zh_l = np.where(z_m == 1, lens, z_hl)[zh_sel]
     work = {
         "zipf": (0, *idx(offs, lens), total),
         "zipf_sorted": (0, *idx(offs[order], lens[order]), total),
         "zipf_crc32": (1, *idx(offs, lens), total),
         "zipf_lt1k": (0, *idx(offs[lt], lens[lt]), int(lens[lt].sum())),
+        "zipf_full": (0, *idx(zf_o, zf_l), int(zf_l.sum())),
+        "zipf_full_asc": (0, *idx(np.sort(zf_o), zf_l), int(zf_l.sum())),
+        "zipf_heads_at": (0, *idx(zh_o, zh_l), int(zh_l.sum())),
         "zipf_heads": (0, *idx(head_o, head_l), int(head_l.sum())),
         "zipf_heads_sorted": (0, *idx(hs_o, hs_l), int(hs_l.sum())),
         "mixed1k": (0, *idx(m1_o, m1_l), int(m1_l.sum())),
