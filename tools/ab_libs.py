@@ -121,6 +121,9 @@ def main(paths):
         # 1M aligned 4 KiB entries through the chunk kernel (one 2 KiB entry keeps them out of the
         # near-uniform gate's band): the chunk loop against the uniform kernel on the same bytes
         "plan4k": (0, *idx(np.arange(n) * 4096, np.where(np.arange(n) == 5, 2048, 4096)), n * 4096 - 2048),
+        # 512 K aligned 8 KiB entries through the chunk kernel: two full chunks each, partials only (no
+        # chunk is final), against u8192_l8 (the uniform kernel on the same 4 GiB)
+        "plan8k": (0, *idx(np.arange(n // 2) * 8192, np.where(np.arange(n // 2) == 5, 4096, 8192)), (n // 2) * 8192 - 4096),
         # 16 entries of 256 MiB: the stream route's inner loop with almost no entry boundary
         "big16": (0, *idx(np.arange(16) * (n * 256), np.full(16, n * 256)), 16 * n * 256),
         # 4096 entries of 1 MiB plus 7 bytes (unaligned ends), packed
