@@ -47,6 +47,9 @@ def metric_for(config: str, algo: str) -> str:
     if config == "zipf":
         return (f"GiB/s {a} over Zipf(1.1) 64 B-64 KiB ledger entries via offset+length index "
                 f"(config 3, device-resident); % HBM peak")
+    if config == "zipf_split":
+        return (f"GiB/s {a} over config 3's Zipf(1.1) 64 B-64 KiB batch split across the GPUs by bytes "
+                f"(strong scaling, device-resident); % HBM peak")
     if config == "indexed4k":
         return f"GiB/s {a} over 4 KiB ledger entries via offset+length index (diagnostic, not the headline)"
     return f"GiB/s {a} ({config})"
@@ -537,7 +540,8 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default=None,
-                    choices=["uniform4k", "shard8m", "zipf", "indexed4k", "host4k", "verify4k", "verify4k_host"],
+                    choices=["uniform4k", "shard8m", "zipf", "zipf_split", "indexed4k", "host4k", "verify4k",
+                             "verify4k_host"],
                     help="default: uniform4k (config 2) at N = 1, shard8m (config 4's 8M x 4 KiB per GPU) at N > 1")
     ap.add_argument("--algo", default="crc32c", choices=["crc32c", "crc32"])
     ap.add_argument("--entries", type=int, default=0, help="entries per GPU (default by config)")
@@ -610,6 +614,7 @@ def run_rank(args, ck, torch, dist, world: int, rank: int, dev) -> None:
         return digest_bench(args, ck, torch, rank, dev, stream, algo)
     if args.config == "verify4k_host":
         return digest_host_bench(args, ck, torch, rank, algo)
+    split = None  # zipf_split: how config 3's one batch is divided over the ranks
     if args.config in ("uniform4k", "shard8m"):
         entry_len = 4096
         n = args.entries or (1 << 20 if args.config == "uniform4k" else 8 << 20)
@@ -639,10 +644,27 @@ def run_rank(args, ck, torch, dist, world: int, rank: int, dev) -> None:
             lens = np.full(n, 4096, dtype=np.int64)
         else:
             offs, lens = zipf_index(n, align=args.zipf_align)
-        total = int(offs[-1] + lens[-1])
-        base = torch.empty(total, dtype=torch.uint8, device=dev)
-        ck.fill_splitmix64(base, 42, first_word=0)
-        d_off = torch.from_numpy(offs).to(dev)
+        if args.config == "zipf_split":
+            from bookkeeper_amd.shard import byte_balanced_bounds, shard_span
+            # config 3's ONE batch split over the ranks by bytes: rank r holds entries
+            # [b[r], b[r+1]) — its span of the global stream, generated in place, and its index rebased
+            bounds = byte_balanced_bounds(lens, world)
+            lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+            if hi <= lo:
+                raise SystemExit(f"zipf_split: rank {rank} has no entries ({n} entries over {world} ranks)")
+            start, end = shard_span(offs, lens, lo, hi, align=128)  # the single-GPU run's line layout
+            split = {"entries_total": n, "bytes_total": int(lens.sum()),
+                     "entries_per_rank": np.diff(bounds).tolist(),
+                     "bytes_per_rank": [int(lens[bounds[r]:bounds[r + 1]].sum()) for r in range(world)]}
+            offs, lens, n = offs[lo:hi] - start, lens[lo:hi], hi - lo
+            base = torch.empty(end - start, dtype=torch.uint8, device=dev)
+            ck.fill_splitmix64(base, 42, first_word=start // 8)
+            total = int(lens.sum())
+        else:
+            total = int(offs[-1] + lens[-1])
+            base = torch.empty(total, dtype=torch.uint8, device=dev)
+            ck.fill_splitmix64(base, 42, first_word=0)
+        d_off = torch.from_numpy(np.ascontiguousarray(offs)).to(dev)
         d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
         out = torch.empty(n, dtype=torch.int32, device=dev)
         payload_bytes = total
@@ -654,6 +676,11 @@ def run_rank(args, ck, torch, dist, world: int, rank: int, dev) -> None:
         kernel_name = "plan pipeline (plan_* + crc_plan_chunks_kernel + plan_combine_kernel)"
         workload = {"workload": f"{n} Zipf(1.1) entries 64 B-64 KiB per GPU (mean {total / n:.0f} B), packed, "
                                 f"{args.algo}", "entries_per_gpu": n, "bytes_per_gpu": total}
+        if split:
+            workload = {"workload": f"config 3: {split['entries_total']} Zipf(1.1) entries 64 B-64 KiB "
+                                    f"({split['bytes_total']} B), packed, split by bytes over {world} GPU"
+                                    f"{'s' if world > 1 else ''} (contiguous entry ranges, strong scaling), "
+                                    f"{args.algo}", **split}
     torch.cuda.synchronize()
 
     # --trace-launches (diagnostic): a HIP event pair on the launch stream around every launch from the
@@ -719,7 +746,9 @@ def run_rank(args, ck, torch, dist, world: int, rank: int, dev) -> None:
                                   shard_check["entries"] if shard_check else 0,
                                   float(shard_check["match"]) if shard_check else 1.0], coll_dev)
 
-    total_payload = payload_bytes * world * args.steps  # every rank processes its batch once per step
+    # weak scaling: every rank processes a batch of its own once per step; zipf_split: the ranks
+    # together process the one batch once per step
+    total_payload = (split["bytes_total"] if split else payload_bytes * world) * args.steps
     value = total_payload / elapsed_max / GIB
     achieved_gbs = algo_bytes / avg_kernel_s / 1e9
     result = {
@@ -731,7 +760,7 @@ def run_rank(args, ck, torch, dist, world: int, rank: int, dev) -> None:
         "warmup": args.warmup,
         "ms_per_step": round(elapsed_max / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if split else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (device-generated splitmix64, seed 42)",
@@ -766,9 +795,9 @@ def run_rank(args, ck, torch, dist, world: int, rank: int, dev) -> None:
             if rank == 0:
                 print(json.dumps(result), flush=True)
             raise SystemExit("PARITY FAILURE: a rank's GPU digests differ from the oracle's")
-    if args.config == "zipf" and world == 1 and not args.no_buckets:
+    if args.config in ("zipf", "zipf_split") and world == 1 and not args.no_buckets:
         result["buckets"] = bucket_rates(ck, torch, algo, base, offs, lens, stream, max(3, args.steps))
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "zipf":
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config in ("zipf", "zipf_split"):
         m = n  # the whole packed batch (6.3 GiB for config 3): well past any cache
         span = int(offs[m - 1] + lens[m - 1])
         host = np.ascontiguousarray(base[:span].cpu().numpy())

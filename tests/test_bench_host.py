@@ -38,8 +38,10 @@ def test_only_config2_carries_the_headline_metric():
     import os
     base = json.load(open(os.path.join(os.path.dirname(bench.__file__), "BASELINE.json")))
     assert bench.metric_for("uniform4k", "crc32c") == base["metric"] == bench.METRIC
-    others = [bench.metric_for(c, a) for c in ("uniform4k", "shard8m", "zipf", "indexed4k") for a in ("crc32c", "crc32")
+    others = [bench.metric_for(c, a) for c in ("uniform4k", "shard8m", "zipf", "zipf_split", "indexed4k")
+              for a in ("crc32c", "crc32")
               if (c, a) != ("uniform4k", "crc32c")]
     assert len(set(others)) == len(others) and base["metric"] not in others
     assert "Zipf" in bench.metric_for("zipf", "crc32") and "CRC32 " in bench.metric_for("zipf", "crc32")
     assert "config 4" in bench.metric_for("shard8m", "crc32c")
+    assert "split across the GPUs by bytes" in bench.metric_for("zipf_split", "crc32c")

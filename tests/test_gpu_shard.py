@@ -166,3 +166,28 @@ def test_bench_two_ranks_default_is_config4_shard(gpu):
     # whole-job value = both ranks' payload over the slowest rank's time
     total = 2 * 8388608 * 4096 * res["steps"] / (1 << 30)
     assert abs(res["value"] - total / (res["ms_per_step"] * res["steps"] / 1e3)) / res["value"] < 0.01
+
+
+def test_bench_zipf_split_by_bytes_two_ranks(gpu):
+    """config 3's one batch over two ranks (gloo, both on this card), contiguous entry
+    ranges balanced by bytes (bookkeeper_amd.shard); strong scaling: value = the batch's bytes per step
+    over the slowest rank's time. Each rank checks 65 536 of its entries against the C oracle."""
+    n = 1 << 18
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--config",
+           "zipf_split", "--entries", str(n), "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert res["n_gpus"] == 2 and res["scaling"] == "strong"
+    cfg = res["config"]
+    assert cfg["entries_total"] == n and sum(cfg["entries_per_rank"]) == n
+    from bench import zipf_index
+    _, lens = zipf_index(n)
+    assert cfg["bytes_total"] == int(lens.sum()) == sum(cfg["bytes_per_rank"])
+    assert max(cfg["bytes_per_rank"]) <= cfg["bytes_total"] / 2 + int(lens.max())
+    assert "split by bytes over 2 GPUs" in cfg["workload"]
+    for p in res["per_gpu"]:
+        assert p["parity_check"] == {"entries": 65536, "match": True}
+    total = cfg["bytes_total"] * res["steps"] / (1 << 30)
+    assert abs(res["value"] - total / (res["ms_per_step"] * res["steps"] / 1e3)) / res["value"] < 0.01

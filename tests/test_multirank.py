@@ -92,3 +92,61 @@ def test_bench_shard_parity_checker_cpu():
     zout = torch.from_numpy(zgood.view(np.int32).copy())
     chk = bench.shard_parity(ck, torch, ck.CRC32, "zipf", torch.from_numpy(zdata.copy()), zout, 200, 0, (offs, lens))
     assert chk == {"entries": 200, "match": True}
+
+
+def _split_worker(rank, world, port, n, q):
+    """One rank of config 3 split by bytes, as bench.py --config zipf_split does it: its entry range
+    from byte_balanced_bounds, its span of the global stream generated from the span's first word,
+    its index rebased to the span; digests by the oracle as the CPU stand-in for its GPU."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch
+    import torch.distributed as dist
+    import oracle
+    from bench import zipf_index
+    from bookkeeper_amd.shard import byte_balanced_bounds, shard_span
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        offs, lens = zipf_index(n)
+        b = byte_balanced_bounds(lens, world)
+        lo, hi = int(b[rank]), int(b[rank + 1])
+        start, end = shard_span(offs, lens, lo, hi, align=128)
+        span = oracle.fill_splitmix64(end - start, 42, start // 8)
+        crcs = oracle.batch(oracle.CRC32C, span, offs[lo:hi] - start, lens[lo:hi])
+        width = int(max(np.diff(b)))
+        mine = torch.full((width,), -1, dtype=torch.int64)
+        mine[:hi - lo] = torch.from_numpy(crcs.astype(np.int64))
+        gathered = [torch.zeros(width, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(gathered, mine)
+        if rank == 0:
+            q.put((b, [g.numpy() for g in gathered]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_zipf_split_by_bytes_equals_unsplit(world):
+    """config 3 over several ranks, contiguous entry ranges balanced by bytes; the
+    ranks' digests, in rank order, are the unsplit batch's."""
+    n = 3000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_split_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    b, parts = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    import oracle
+    from bench import zipf_index
+    offs, lens = zipf_index(n)
+    whole = oracle.fill_splitmix64(int(offs[-1] + lens[-1]), 42)
+    want = oracle.batch(oracle.CRC32C, whole, offs, lens)
+    got = np.concatenate([parts[r][:b[r + 1] - b[r]] for r in range(world)]).astype(np.uint32)
+    assert got.size == n and (got == want).all()
+    per = [int(lens[b[r]:b[r + 1]].sum()) for r in range(world)]
+    assert max(per) <= lens.sum() / world + lens.max()
