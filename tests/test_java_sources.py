@@ -60,10 +60,13 @@ def _ref_class_file(fqcn):
     return None
 
 
-def _package_has(pkg, name):
+def _package_has(pkg, name, tests=False):
+    """A class of pkg in the reference's main sources or native/java; with tests, also the reference's
+    test sources (the JUnit tests under native/java-test sit beside them)."""
     rel = os.path.join(*pkg.split("."), name + ".java")
-    return bool(glob.glob(os.path.join(REF, "**", "src", "main", "java", rel), recursive=True)) or os.path.exists(
-        os.path.join(JAVA, rel))
+    trees = ("main", "test") if tests else ("main",)
+    return any(glob.glob(os.path.join(REF, "**", "src", t, "java", rel), recursive=True) for t in trees) or \
+        os.path.exists(os.path.join(JAVA, rel))
 
 
 @pytest.mark.parametrize("path", _sources() if os.path.isdir(REF) else [], ids=os.path.basename)
@@ -84,7 +87,8 @@ def test_imports_resolve(path):
     used |= set(re.findall(r"(?<![\w.])([A-Z]\w*)\.[a-zA-Z_]", body))
     declared = set(re.findall(r"\b(?:class|interface)\s+([A-Z]\w*)", body))
     for name in sorted(used - imported - declared - JAVA_LANG):
-        assert _package_has(pkg, name), f"{os.path.basename(path)}: {name} is not a class of {pkg}"
+        assert _package_has(pkg, name, tests=path.startswith(JAVA_TEST)), \
+            f"{os.path.basename(path)}: {name} is not a class of {pkg}"
 
 
 def test_gpu_int_hash_implements_every_int_hash_method():
@@ -131,6 +135,8 @@ MEMBERS = [
     ("org.apache.bookkeeper.proto.BookieProtocol", r"int MASTER_KEY_LENGTH = 20;"),
     ("org.apache.bookkeeper.util.ByteBufList", r"public static ByteBufList get\(ByteBuf b1, ByteBuf b2\)"),
     ("org.apache.bookkeeper.client.LedgerHandle", r"\n    final ClientContext clientCtx;"),
+    # native/java-test/.../GpuIntHashTest.java
+    ("com.scurrilous.circe.checksum.Crc32cIntChecksum", r"public static int computeChecksum\(ByteBuf payload\)"),
     # native/java-test/.../GpuBatchHooksTest.java
     ("org.apache.bookkeeper.util.ByteBufList", r"public byte\[\] toArray\(\)"),
     ("org.apache.bookkeeper.util.ByteBufList", r"public static ByteBufList get\(\)"),
