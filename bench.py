@@ -112,7 +112,7 @@ def gather_over_ranks(values: list[float], device=None) -> list[list[float]]:
     """Every rank's timing values (all_gather of a few floats; timing only, never CRC data)."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return [list(values)]
     t = torch.tensor(values, dtype=torch.float64, device=device)
     out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
@@ -130,7 +130,7 @@ def gather_identity(dev, world: int) -> list[dict]:
             "pci": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}",
             "uuid": str(getattr(p, "uuid", "")),
             "world_size_seen": dist.get_world_size() if (dist.is_available() and dist.is_initialized()) else 1}
-    if world == 1 or not (dist.is_available() and dist.is_initialized()):
+    if not (dist.is_available() and dist.is_initialized()):
         return [mine]
     out = [None] * dist.get_world_size()
     dist.all_gather_object(out, mine)
@@ -141,7 +141,7 @@ def max_over_ranks(value: float, device=None) -> float:
     """Whole-job time = the slowest rank's (all_reduce MAX; the only cross-rank traffic)."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return float(value)
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -580,7 +580,11 @@ def main() -> None:
         raise SystemExit(f"LOCAL_RANK {local} but only {ndev} visible GPUs")
     dev = torch.device("cuda", local % ndev)  # % only matters for a gloo rehearsal on fewer GPUs
     torch.cuda.set_device(dev)
-    if world > 1:
+    # a process group whenever torch.distributed.run started this process, a world of one included
+    # (its RCCL communicator then runs the same barriers and collectives as N > 1); a plain
+    # `python bench.py` at N = 1 (the driver's headline command) has none
+    grouped = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ
+    if grouped:
         if args.dist_backend == "nccl":
             # RCCL; device_id binds this rank's communicator to its GPU up front (no lazy init on the
             # first collective). Only timing crosses ranks: barriers, one MAX, one all_gather.
@@ -590,7 +594,7 @@ def main() -> None:
     try:
         run_rank(args, ck, torch, dist, world, rank, dev)
     finally:  # every exit path, a parity failure's SystemExit included
-        if world > 1 and dist.is_initialized():
+        if grouped and dist.is_initialized():
             dist.destroy_process_group()
 
 
@@ -719,7 +723,8 @@ def run_rank(args, ck, torch, dist, world: int, rank: int, dev) -> None:
     # HIP events on the launch stream bracket the K back-to-back launches (no event packets between
     # launches); the average launch duration is their span / K
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
+    grouped = dist.is_available() and dist.is_initialized()
+    if grouped:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -728,7 +733,7 @@ def run_rank(args, ck, torch, dist, world: int, rank: int, dev) -> None:
         traced(step)
     ev1.record(stream)
     torch.cuda.synchronize()
-    if world > 1:
+    if grouped:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     avg_kernel_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
