@@ -654,8 +654,8 @@ def run_rank(args, ck, torch, dist, world: int, rank: int, dev) -> None:
             # [b[r], b[r+1]) — its span of the global stream, generated in place, and its index rebased
             bounds = byte_balanced_bounds(lens, world)
             lo, hi = int(bounds[rank]), int(bounds[rank + 1])
-            if hi <= lo:
-                raise SystemExit(f"zipf_split: rank {rank} has no entries ({n} entries over {world} ranks)")
+            if (np.diff(bounds) == 0).any():  # the same test on every rank: all of them stop together
+                raise SystemExit(f"zipf_split: a rank would have no entries ({n} entries over {world} ranks)")
             start, end = shard_span(offs, lens, lo, hi, align=128)  # the single-GPU run's line layout
             split = {"entries_total": n, "bytes_total": int(lens.sum()),
                      "entries_per_rank": np.diff(bounds).tolist(),
