@@ -61,10 +61,11 @@ public final class GpuBatchPackager {
         }
         final int algo = dm instanceof CRC32CDigestManager ? GpuDigest.CRC32C
                 : dm instanceof CRC32DigestManager ? GpuDigest.CRC32 : -1;
-        if (n == 0 || algo < 0 || !GpuDigest.isLoaded()) {
+        final int frameLen = DigestManager.METADATA_LENGTH + dm.macCodeLength;
+        // (the frames buffer below is sized n * frameLen bytes: int arithmetic)
+        if (n == 0 || (long) n * frameLen > Integer.MAX_VALUE || algo < 0 || !GpuDigest.isLoaded()) {
             return perEntry(dm, entryIds, lastAddConfirmed, lengths, payloads, masterKey, flags);
         }
-        final int frameLen = DigestManager.METADATA_LENGTH + dm.macCodeLength;
         // [32 B header][digest] per entry, back to back, and the u32 digests (direct, little-endian)
         final ByteBuf frames = PooledByteBufAllocator.DEFAULT.directBuffer(n * frameLen);
         final ByteBuf digests = PooledByteBufAllocator.DEFAULT.directBuffer(4 * n);

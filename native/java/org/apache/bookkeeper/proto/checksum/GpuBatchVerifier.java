@@ -51,7 +51,8 @@ public final class GpuBatchVerifier {
         final int n = bufList.size();
         final int algo = dm instanceof CRC32CDigestManager ? GpuDigest.CRC32C
                 : dm instanceof CRC32DigestManager ? GpuDigest.CRC32 : -1;
-        boolean direct = n > 0 && algo >= 0 && GpuDigest.isLoaded();
+        // (the per-entry index buffers below are sized 8 * n bytes: int arithmetic)
+        boolean direct = n > 0 && n <= Integer.MAX_VALUE / 8 && algo >= 0 && GpuDigest.isLoaded();
         for (int i = 0; direct && i < n; i++) {
             final ByteBuf b = bufList.getBuffer(i);
             // the reference's absolute addressing equals the frame [memoryAddress(), + readableBytes())
