@@ -1154,11 +1154,44 @@ __device__ __forceinline__ void chunk_prefetch(const uint8_t* __restrict__ base,
     }
 }
 
+#ifndef BKD_FIRST_FAST
+// The chunk kernel's step-0 masks, seed image and pad removal as clamped shifts, no branches: bit 0
+// its short tail, bit 1 its long loop (0: the branchy form). 1M one-step chunks -6 %, the < 1 KiB
+// bucket -3.7 %, config 3 -0.3 % (round 6, profiles/r08b_ab_first_block_fast.log)
+#define BKD_FIRST_FAST 3
+#endif
+// Dword k of a chunk's step-0 block, branch-free: x8 = 8 * (d0 - 4k) bits of it lie in front of the
+// chunk's first byte (cleared: low32(~0 << clamp(x8, 0, 32))), and it takes its part of the seed
+// image r0 << 8*d0 (low32((r0 : 0) >> (32 - clamp(x8, -32, 32))); a shift of 64 is 0 mod 64 and the
+// low half of (r0 : 0) is zero). The same part with x8 = 8 * (d0 - step) is the spill into step 1.
+__device__ __forceinline__ uint32_t seed_part(uint32_t r0, int32_t x8) {
+    const uint32_t sh = (uint32_t)(32 - min(max(x8, -32), 32));
+    return (uint32_t)(((uint64_t)r0 << 32) >> (sh & 63u));
+}
+__device__ __forceinline__ uint32_t keep_from(uint32_t x, int32_t x8) {  // bytes at or past x8 / 8
+    return x & (uint32_t)(~0ull << (uint32_t)min(max(x8, 0), 32));
+}
+__device__ __forceinline__ u32x4 first_block_fast(u32x4 W0, uint32_t r0, int32_t d0) {
+    const int32_t x8 = 8 * d0;
+    return u32x4{keep_from(W0.x, x8) ^ seed_part(r0, x8), keep_from(W0.y, x8 - 32) ^ seed_part(r0, x8 - 32),
+                 keep_from(W0.z, x8 - 64) ^ seed_part(r0, x8 - 64), keep_from(W0.w, x8 - 96) ^ seed_part(r0, x8 - 96)};
+}
+// The bytes of a chunk's last block at or past `keep` (the pad folded last, XORed out again).
+__device__ __forceinline__ u32x4 pad_junk_fast(u32x4 last, int32_t keep) {
+    const int32_t x8 = 8 * keep;
+    return u32x4{keep_from(last.x, x8), keep_from(last.y, x8 - 32), keep_from(last.z, x8 - 64),
+                 keep_from(last.w, x8 - 96)};
+}
+
 // The lane's step-0 block of chunk `c` with the bytes in front of the chunk cleared and the seed
 // image XORed in; fx = the part of the seed image that spills into step 1's dword 0.
 template <int G>
 __device__ __forceinline__ u32x4 chunk_first_block(const ChunkGeo& c, u32x4 W0, uint32_t& fx) {
     using Gm = Geo<G>;
+#if BKD_FIRST_FAST & 1
+    fx = seed_part(c.r0, 8 * (c.d0 - Gm::kStep));
+    return first_block_fast(W0, c.r0, c.d0);
+#endif
     const int32_t d0 = c.d0;
     u32x4 w;
     if (d0 <= 0) w = W0;
@@ -1205,7 +1238,11 @@ __device__ __forceinline__ uint32_t short_chunk_fold(const uint32_t* lds, uint32
 #pragma unroll
         for (int k = 0; k < PF; ++k)
             if ((uint32_t)k + 1u == rem) last = A[k];
+#if BKD_FIRST_FAST & 1
+        const u32x4 junk = pad_junk_fast(last, c.keep);
+#else
         const u32x4 junk = c.keep <= 0 ? last : mask_low_bytes(last, (uint32_t)c.keep);
+#endif
         c0 ^= junk.x;
         c1 ^= junk.y;
         c2 ^= junk.z;
@@ -1232,6 +1269,10 @@ __device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lan
     // paying one each
     chunk_prefetch<G, PF, NT>(base, nx, NW0, NA);
 #endif
+#if BKD_FIRST_FAST & 2
+    const u32x4 w = first_block_fast(W0, c.r0, d0);
+    uint32_t fx = seed_part(c.r0, 8 * (d0 - Gm::kStep));
+#else
     u32x4 w;
     if (d0 <= 0) w = W0;
     else if (d0 < 16) w = mask_low_bytes(W0, (uint32_t)d0);
@@ -1251,6 +1292,7 @@ __device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lan
     }
     uint32_t fx = 0u;
     if (d0 > Gm::kStep - 4) fx = place_seed(r0, d0 - Gm::kStep);
+#endif
     uint32_t c0 = w.x, c1 = w.y, c2 = w.z, c3 = w.w;
     // the lane's last block as it was folded: a pad is XORed out of the very register that folded
     // it, so the bytes past the entry (another entry's, or past the caller's buffer) cancel whatever
@@ -1339,7 +1381,11 @@ __device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lan
         // the last step's block of this lane ends past the entry: its bytes >= the entry's end were
         // folded last (XORed in after the final multiply), so XOR them out again
         const int32_t keep = c.keep;
+#if BKD_FIRST_FAST & 2
+        const u32x4 junk = pad_junk_fast(last, keep);
+#else
         const u32x4 junk = keep <= 0 ? last : mask_low_bytes(last, (uint32_t)keep);
+#endif
         c0 ^= junk.x;
         c1 ^= junk.y;
         c2 ^= junk.z;
