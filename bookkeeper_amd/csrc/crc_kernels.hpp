@@ -1154,6 +1154,14 @@ __device__ __forceinline__ void chunk_prefetch(const uint8_t* __restrict__ base,
     }
 }
 
+#ifndef BKD_HOLE_GEO
+// The chunk kernel requests every geometry's blocks as they are: a hole has a window at base[0]
+// (skip_desc) and a chunk past the list the last real chunk's, so no geometry is selected per chunk
+// (0: the field-by-field selects of a "last real chunk" geometry). The < 1 KiB bucket -2.1 %,
+// 1M one-step chunks -1.6 %, 8 KiB chunk pairs -0.6 %, config 3 +-0, and the short tail's one
+// spilled register gone (round 6, profiles/r08h_ab_hole_geometry_full_static.log)
+#define BKD_HOLE_GEO 1
+#endif
 #ifndef BKD_FIRST_FAST
 // The chunk kernel's step-0 masks, seed image and pad removal as clamped shifts, no branches: bit 0
 // its short tail, bit 1 its long loop (0: the branchy form). 1M one-step chunks -6 %, the < 1 KiB
@@ -1418,6 +1426,11 @@ __device__ __forceinline__ void short_chunks_loop(const uint32_t* lds, uint32_t 
         if (j >= n) c.len = 0;
         return c;
     };
+#if BKD_HOLE_GEO
+    // every geometry has loadable blocks: a chunk past the list has the last real chunk's (clampi), a
+    // hole the window skip_desc() gives it at base[0]
+    auto load = [&](const ChunkGeo& c, u32x4& W0, u32x4 (&A)[PF]) { chunk_prefetch<G, PF, NT>(base, c, W0, A); };
+#else
     // blocks a hole (or a chunk past the list) loads instead: the last real chunk's, base[0, 16)
     // before one is seen. Selected field by field: a reference to one of two geometries would put
     // both in scratch memory.
@@ -1435,6 +1448,7 @@ __device__ __forceinline__ void short_chunks_loop(const uint32_t* lds, uint32_t 
         t.J = fJ;
         chunk_prefetch<G, PF, NT>(base, t, W0, A);
     };
+#endif
     u32x4 W0x, Ax[PF], W0y, Ay[PF], W0z, Az[PF];
     ChunkGeo cx = geo_at(i), cy = geo_at(i + ngroups), cz = geo_at(i + 2 * ngroups);
     load(cx, W0x, Ax);
@@ -1512,17 +1526,25 @@ __device__ __forceinline__ void long_chunks_loop(const uint32_t* lds, uint32_t l
     // load), and enough loads issued between a descriptor and its use that the compiler's count of
     // them never reaches back into the current chunk's prefetch.
     PlanDesc dA = descs[clampi(i + ngroups)], dB = descs[clampi(i + 2 * ngroups)];
+#if BKD_HOLE_GEO
+    // every geometry has loadable blocks (a hole's window is base[0], skip_desc; a missing next chunk
+    // is the last real one, clampi): the next chunk's blocks are requested whatever it is
+#define BKD_PF_GEO(nx, cur) (nx)
+    chunk_prefetch<G, PF, NT>(base, cur, W0x, Ax);
+#else
     // a hole's prefetch reads base[0, 16) (only plans that overflowed their capacity have holes)
     ChunkGeo safe;
     safe.la0 = safe.a = 0, safe.J = 1;
+#define BKD_PF_GEO(nx, cur) pf_geo(nx, cur.len ? cur : safe)
     chunk_prefetch<G, PF, NT>(base, cur.len ? cur : safe, W0x, Ax);
+#endif
 #define BKD_CHUNK_HALF(DN, W0C, AC, BC, W0N, AN)                                                            \
     {                                                                                                      \
         const bool more = i + ngroups < n;                                                                 \
         ChunkGeo nx = chunk_geo<G>(DN, g);                                                                 \
         DN = descs[clampi(i + 3 * ngroups)];                                                               \
         if (!more) nx.len = 0;                                                                             \
-        const ChunkGeo& pg = pf_geo(nx, cur.len ? cur : safe);                                             \
+        const ChunkGeo& pg = BKD_PF_GEO(nx, cur);                                                          \
         const uint32_t v = cur.len ? chunk_fold<G, PF, NT>(lds, lanereg, g, base, cur, W0C, AC, BC, pg, W0N, AN) \
                                    : (chunk_prefetch<G, PF, NT>(base, pg, W0N, AN), 0u);                   \
         emit(cur, v);                                                                                      \
@@ -1551,6 +1573,7 @@ __device__ __forceinline__ void long_chunks_loop(const uint32_t* lds, uint32_t l
     held.finish(g, partials, gid, ngroups, n);
 #endif
 #undef BKD_CHUNK_HALF
+#undef BKD_PF_GEO
 }
 
 // Blocks per chunk in the short tail's register sets beside step 0: chunks of <= kShortPF + 1 steps

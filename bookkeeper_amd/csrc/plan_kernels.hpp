@@ -133,7 +133,11 @@ __device__ __forceinline__ PlanDesc chunk_desc(const EntryPlan& p, uint32_t c, u
     return d;
 }
 
-__device__ __forceinline__ PlanDesc skip_desc() { return PlanDesc{0ull, 0u, 0u}; }
+// A hole (an entry past the plan's capacity, computed by the overflow tail instead): no bytes, and a
+// window at base[0] so that the chunk kernel may request its blocks like any chunk's (base[16g],
+// within the first 16 * G bytes: a plan only overflows with multi-chunk entries, so base holds more
+// than one chunk then).
+__device__ __forceinline__ PlanDesc skip_desc() { return PlanDesc{(uint64_t)kWBias, 0u, 0u}; }
 
 // Deterministic block-wide exclusive scan (1024 threads = 16 waves).
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t& total) {
