@@ -125,6 +125,29 @@ __device__ __forceinline__ bool lds_image_at_zero(const uint32_t* lds) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t*)lds == 0u;
 }
 
+// One fold step of the four streams with all 16 lookups requested before any is used, through the
+// compiler's own LDS addressing (so valid wherever the image sits; its waits are counted): the
+// scheduling barriers keep the 16 address perms, then the 16 reads, then the XORs together.
+__device__ __forceinline__ void fold4_grouped(const uint32_t* lds, uint32_t& c0, uint32_t& c1, uint32_t& c2,
+                                              uint32_t& c3, uint32_t lanereg, uint32_t d0, uint32_t d1, uint32_t d2,
+                                              uint32_t d3) {
+    uint32_t t[16];
+    const uint32_t cs[4] = {c0, c1, c2, c3};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        t[4 * k + 0] = lds_word(lds, __builtin_amdgcn_perm(cs[k], lanereg, 0x0C0C0400u));
+        t[4 * k + 1] = lds_word(lds, __builtin_amdgcn_perm(cs[k], lanereg, 0x0C0C0500u) + 128u);
+        t[4 * k + 2] = lds_word(lds, __builtin_amdgcn_perm(cs[k], lanereg, 0x0C020600u));
+        t[4 * k + 3] = lds_word(lds, __builtin_amdgcn_perm(cs[k], lanereg, 0x0C020700u) + 128u);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x0002, 16, 0);  // the 16 address perms (VALU)
+    __builtin_amdgcn_sched_group_barrier(0x0100, 16, 0);  // the 16 reads (DS read)
+    c0 = xor3(xor3(t[0], t[1], t[2]), t[3], d0);
+    c1 = xor3(xor3(t[4], t[5], t[6]), t[7], d1);
+    c2 = xor3(xor3(t[8], t[9], t[10]), t[11], d2);
+    c3 = xor3(xor3(t[12], t[13], t[14]), t[15], d3);
+}
+
 __device__ __forceinline__ void fold4_main(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t lanereg,
                                            uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3) {
     uint32_t t[16];
@@ -1154,6 +1177,13 @@ __device__ __forceinline__ void chunk_prefetch(const uint8_t* __restrict__ base,
     }
 }
 
+#ifndef BKD_SHORT_FOLD4
+// The short tail's folds with a step's 16 lookups requested before any is used (fold4_grouped; the
+// compiler's own schedule waited stream by stream there): two- and four-step chunks -0.9 / -2.6 %,
+// the < 1 KiB bucket -0.8 %, config 3 -0.1 % (round 6, profiles/r08o_ab_short_fold_grouped.log; the
+// inline-asm fold4_main, which needs the image at LDS address 0, measured alike: r08n_*)
+#define BKD_SHORT_FOLD4 1
+#endif
 #ifndef BKD_HOLE_GEO
 // The chunk kernel requests every geometry's blocks as they are: a hole has a window at base[0]
 // (skip_desc) and a chunk past the list the last real chunk's, so no geometry is selected per chunk
@@ -1235,10 +1265,14 @@ __device__ __forceinline__ uint32_t short_chunk_fold(const uint32_t* lds, uint32
 #pragma unroll
     for (int k = 0; k < PF; ++k) {
         if ((uint32_t)k < rem) {
+#if BKD_SHORT_FOLD4
+            fold4_grouped(lds, c0, c1, c2, c3, lanereg, A[k].x ^ (k == 0 ? fx : 0u), A[k].y, A[k].z, A[k].w);
+#else
             c0 = mul_main_add(lds, c0, lanereg, A[k].x ^ (k == 0 ? fx : 0u));
             c1 = mul_main_add(lds, c1, lanereg, A[k].y);
             c2 = mul_main_add(lds, c2, lanereg, A[k].z);
             c3 = mul_main_add(lds, c3, lanereg, A[k].w);
+#endif
         }
     }
     if (c.pad && c.keep < 16) {  // the last step's bytes past the entry were folded last: XOR them out
