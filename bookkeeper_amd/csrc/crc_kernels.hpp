@@ -1202,6 +1202,7 @@ __device__ __forceinline__ void chunk_prefetch(const uint8_t* __restrict__ base,
 // chunk's first byte (cleared: low32(~0 << clamp(x8, 0, 32))), and it takes its part of the seed
 // image r0 << 8*d0 (low32((r0 : 0) >> (32 - clamp(x8, -32, 32))); a shift of 64 is 0 mod 64 and the
 // low half of (r0 : 0) is zero). The same part with x8 = 8 * (d0 - step) is the spill into step 1.
+// (tests/test_first_block_model.py pins both to the branchy form, every d0 and keep in [-1100, 1100].)
 __device__ __forceinline__ uint32_t seed_part(uint32_t r0, int32_t x8) {
     const uint32_t sh = (uint32_t)(32 - min(max(x8, -32), 32));
     return (uint32_t)(((uint64_t)r0 << 32) >> (sh & 63u));
