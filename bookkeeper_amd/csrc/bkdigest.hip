@@ -400,20 +400,25 @@ int dispatch_lanes(DeviceState& ds, int lanes, int algo, const uint8_t* base, co
 }
 
 template <int G>
-void launch_plan_chunks(const bkd::PlanRun& run, const uint8_t* base, const bkd::PlanDesc* descs,
-                        const uint32_t* count, const uint32_t* tab,
+void launch_plan_chunks(const bkd::PlanRun& run, const uint8_t* base, const bkd::PlanDesc* descs, bool d8,
+                        uint32_t r0h, const uint32_t* count, const uint32_t* tab,
                         uint32_t* out, uint32_t* partials, const bkd::PlanDirectSrc& ov, int blocks, hipStream_t st,
                         uint32_t* err, int pf) {
-    // pf: read once by launch_plan (one value per call)
+    // pf: read once by launch_plan (one value per call); d8 (PlanDesc8) only with the default pf
     if (pf == 8)
         hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 8, kNT, bkd::PlanDirectSrc>), dim3((unsigned)blocks),
-                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err);
+                           dim3(bkd::kBlock), 0, st, base, descs, r0h, count, tab, out, partials, ov, run, err);
     else if (pf == 4)
         hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 4, kNT, bkd::PlanDirectSrc>), dim3((unsigned)blocks),
-                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err);
+                           dim3(bkd::kBlock), 0, st, base, descs, r0h, count, tab, out, partials, ov, run, err);
+    else if (d8)
+        hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 2, kNT, bkd::PlanDirectSrc, bkd::PlanDesc8>),
+                           dim3((unsigned)blocks), dim3(bkd::kBlock), 0, st, base,
+                           reinterpret_cast<const bkd::PlanDesc8*>(descs), r0h, count, tab, out, partials, ov, run,
+                           err);
     else
         hipLaunchKernelGGL((bkd::crc_plan_chunks_kernel<G, 2, kNT, bkd::PlanDirectSrc>), dim3((unsigned)blocks),
-                           dim3(bkd::kBlock), 0, st, base, descs, count, tab, out, partials, ov, run, err);
+                           dim3(bkd::kBlock), 0, st, base, descs, r0h, count, tab, out, partials, ov, run, err);
 }
 
 // Indexed batch through the chunked plan (plan_kernels.hpp): five stream-ordered kernels, no
@@ -442,6 +447,12 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
 #endif
     const int pf = g_plan_pf.load();
     pg.jshort = BKD_SHORT_TAIL ? (uint32_t)bkd::kShortPF + 1u : 0u;
+    // 8-byte descriptors when the batch has one seed for every entry (its head register is then a
+    // kernel argument) and the default loads in flight (PlanDesc8, crc_kernels.hpp)
+#ifndef BKD_PLAN_D8
+#define BKD_PLAN_D8 1
+#endif
+    pg.d8 = (BKD_PLAN_D8 && seeds == nullptr && size < bkd::kPlanMaxSize8 && pf == 2) ? 1u : 0u;
     pg.nbins = (pg.ch + pg.merge - 1u + pg.step - 1u) / pg.step + 1u;
     pg.step_sh = (uint32_t)__builtin_ctz(pg.step);
     pg.ch_sh = (pg.ch & (pg.ch - 1u)) == 0u ? (uint32_t)__builtin_ctz(pg.ch) : 0xFFu;
@@ -525,11 +536,11 @@ int launch_plan(DeviceState& ds, int algo, const uint8_t* base, uint64_t size, c
     const uint32_t* tab = ds.tables[algo][lane_index(G)];
     const bkd::PlanDirectSrc ov{n, offsets, lengths, seeds, seed_all, size, out, pslot, hdr, capacity, false};
     switch (G) {
-        case 4: launch_plan_chunks<4>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
-        case 8: launch_plan_chunks<8>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
-        case 16: launch_plan_chunks<16>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
-        case 32: launch_plan_chunks<32>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
-        default: launch_plan_chunks<64>(run, base, descs, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
+        case 4: launch_plan_chunks<4>(run, base, descs, pg.d8 != 0u, ~seed_all, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
+        case 8: launch_plan_chunks<8>(run, base, descs, pg.d8 != 0u, ~seed_all, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
+        case 16: launch_plan_chunks<16>(run, base, descs, pg.d8 != 0u, ~seed_all, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
+        case 32: launch_plan_chunks<32>(run, base, descs, pg.d8 != 0u, ~seed_all, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
+        default: launch_plan_chunks<64>(run, base, descs, pg.d8 != 0u, ~seed_all, hdr + bkd::kHdrWork, tab, out, partials, ov, ds.cus, st, err, pf); break;
     }
     const uint32_t* btab = tab + bkd::gf2::byte_table_offset(G);
     hipLaunchKernelGGL(bkd::plan_combine_kernel, dim3(std::min(nb * reps, pgrid)), dim3(1024), 0, st, base, offsets, lengths, seeds,

@@ -1128,6 +1128,16 @@ struct __attribute__((aligned(16))) PlanDesc {
     uint32_t dst;
 };
 
+// The 8-byte descriptor of an unseeded batch (no per-entry seeds; base < kPlanMaxSize8): the same
+// window / pad / length word, bit 40 set on a head (its register is the batch's one ~seed, a kernel
+// argument), and every chunk's partial at its own list position (no final chunks: the combine
+// finishes single-chunk entries too). Half the descriptor bytes the plan writes and reads back.
+struct __attribute__((aligned(8))) PlanDesc8 {
+    uint64_t s_len;
+};
+constexpr int kPlanHeadBit = 40;
+constexpr uint64_t kPlanMaxSize8 = (1ull << kPlanHeadBit) - 4096u;  // W + kWBias below bit 40
+
 // ---- pipelined chunk processing for the plan -------------------------------------------
 // A chunk's first PF+1 steps are loaded while the PREVIOUS chunk of the group is still being
 // folded and finalised, so a group never waits a full HBM latency at a chunk boundary. Two
@@ -1148,7 +1158,7 @@ struct ChunkGeo {
 };
 
 template <int G>
-__device__ __forceinline__ ChunkGeo chunk_geo(const PlanDesc& d, int g) {
+__device__ __forceinline__ ChunkGeo chunk_geo(const PlanDesc& d, int g, uint32_t /*r0h: PlanDesc8 only*/ = 0u) {
     using Gm = Geo<G>;
     ChunkGeo c;
     const int64_t w = (int64_t)(d.s_len & ((1ull << kPlanOffBits) - 1u)) - kWBias;
@@ -1163,6 +1173,15 @@ __device__ __forceinline__ ChunkGeo chunk_geo(const PlanDesc& d, int g) {
     c.r0 = d.r0;
     c.dst = d.dst;
     return c;
+}
+
+template <int G>
+__device__ __forceinline__ ChunkGeo chunk_geo(const PlanDesc8& d, int g, uint32_t r0h) {
+    PlanDesc full;
+    full.s_len = d.s_len & ~(1ull << kPlanHeadBit);
+    full.r0 = ((d.s_len >> kPlanHeadBit) & 1u) ? r0h : 0u;
+    full.dst = 0u;
+    return chunk_geo<G>(full, g);
 }
 
 // Loads of step 0 and steps 1..PF of chunk c (addresses past the chunk clamp to a valid block).
@@ -1444,9 +1463,10 @@ __device__ __forceinline__ uint32_t chunk_fold(const uint32_t* lds, uint32_t lan
 // chunk. Here three register sets rotate: a chunk's blocks are requested three chunks before its
 // fold and its descriptor three chunks before that. Every load is unconditional (a hole or a chunk
 // past the list re-reads a real chunk's blocks), so the compiler's waits can count exactly.
-template <int G, int PF, bool NT>
+template <int G, int PF, bool NT, class Desc>
 __device__ __forceinline__ void short_chunks_loop(const uint32_t* lds, uint32_t lanereg, int g,
-                                                  const uint8_t* __restrict__ base, const PlanDesc* __restrict__ descs,
+                                                  const uint8_t* __restrict__ base, const Desc* __restrict__ descs,
+                                                  uint32_t r0h,
                                                   uint64_t i, uint64_t n, uint64_t ngroups, uint32_t* __restrict__ out,
                                                   uint32_t* __restrict__ partials, uint64_t nstart) {
 #if BKD_HOLD_SHORT > 0
@@ -1457,7 +1477,7 @@ __device__ __forceinline__ void short_chunks_loop(const uint32_t* lds, uint32_t 
 #endif
     auto clampi = [&](uint64_t j) { return j < n ? j : n - 1; };
     auto geo_at = [&](uint64_t j) {
-        ChunkGeo c = chunk_geo<G>(descs[clampi(j)], g);
+        ChunkGeo c = chunk_geo<G>(descs[clampi(j)], g, r0h);
         if (j >= n) c.len = 0;
         return c;
     };
@@ -1489,8 +1509,8 @@ __device__ __forceinline__ void short_chunks_loop(const uint32_t* lds, uint32_t 
     load(cx, W0x, Ax);
     load(cy, W0y, Ay);
     load(cz, W0z, Az);
-    PlanDesc dx = descs[clampi(i + 3 * ngroups)], dy = descs[clampi(i + 4 * ngroups)],
-             dz = descs[clampi(i + 5 * ngroups)];
+    Desc dx = descs[clampi(i + 3 * ngroups)], dy = descs[clampi(i + 4 * ngroups)],
+         dz = descs[clampi(i + 5 * ngroups)];
 #if BKD_HOLD_SHORT > 0
 #define BKD_SHORT_EMIT(C, v)                                                                 \
     held.put(v, g, partials + nstart, gid0, ngroups, n - nstart);                            \
@@ -1506,7 +1526,7 @@ __device__ __forceinline__ void short_chunks_loop(const uint32_t* lds, uint32_t 
     {                                                                                        \
         const uint32_t v = C.len ? short_chunk_fold<G, PF>(lds, lanereg, C, W0C, AC) : 0u;   \
         BKD_SHORT_EMIT(C, v)                                                                 \
-        C = chunk_geo<G>(DC, g); /* chunk i + 3 ngroups */                                   \
+        C = chunk_geo<G>(DC, g, r0h); /* chunk i + 3 ngroups */                              \
         if (i + 3 * ngroups >= n) C.len = 0;                                                 \
         load(C, W0C, AC);                                                                    \
         DC = descs[clampi(i + 6 * ngroups)];                                                 \
@@ -1528,9 +1548,10 @@ __device__ __forceinline__ void short_chunks_loop(const uint32_t* lds, uint32_t 
 }
 
 // Chunks [0, n) of the list in grid stride, one prefetched chunk per group (X/Y sets).
-template <int G, int PF, bool NT>
+template <int G, int PF, bool NT, class Desc>
 __device__ __forceinline__ void long_chunks_loop(const uint32_t* lds, uint32_t lanereg, int g,
-                                                 const uint8_t* __restrict__ base, const PlanDesc* __restrict__ descs,
+                                                 const uint8_t* __restrict__ base, const Desc* __restrict__ descs,
+                                                 uint32_t r0h,
                                                  uint64_t n, uint64_t gid, uint64_t ngroups, uint32_t* __restrict__ out,
                                                  uint32_t* __restrict__ partials) {
     auto clampi = [&](uint64_t j) { return j < n ? j : n - 1; };
@@ -1554,13 +1575,13 @@ __device__ __forceinline__ void long_chunks_loop(const uint32_t* lds, uint32_t l
 
     u32x4 W0x, Ax[PF], Bx[PF], W0y, Ay[PF], By[PF];
     uint64_t i = gid;
-    ChunkGeo cur = chunk_geo<G>(descs[i], g);
+    ChunkGeo cur = chunk_geo<G>(descs[i], g, r0h);
     // Descriptors of the next chunk of each half live in their own registers (dA for set-X halves,
     // dB for set-Y halves), each loaded two halves before its use and reloaded (three rounds ahead)
     // right after: no copy of a just-loaded value (a `dn = dnn` copy made the compiler wait for that
     // load), and enough loads issued between a descriptor and its use that the compiler's count of
     // them never reaches back into the current chunk's prefetch.
-    PlanDesc dA = descs[clampi(i + ngroups)], dB = descs[clampi(i + 2 * ngroups)];
+    Desc dA = descs[clampi(i + ngroups)], dB = descs[clampi(i + 2 * ngroups)];
 #if BKD_HOLE_GEO
     // every geometry has loadable blocks (a hole's window is base[0], skip_desc; a missing next chunk
     // is the last real one, clampi): the next chunk's blocks are requested whatever it is
@@ -1576,7 +1597,7 @@ __device__ __forceinline__ void long_chunks_loop(const uint32_t* lds, uint32_t l
 #define BKD_CHUNK_HALF(DN, W0C, AC, BC, W0N, AN)                                                            \
     {                                                                                                      \
         const bool more = i + ngroups < n;                                                                 \
-        ChunkGeo nx = chunk_geo<G>(DN, g);                                                                 \
+        ChunkGeo nx = chunk_geo<G>(DN, g, r0h);                                                            \
         DN = descs[clampi(i + 3 * ngroups)];                                                               \
         if (!more) nx.len = 0;                                                                             \
         const ChunkGeo& pg = BKD_PF_GEO(nx, cur);                                                          \
@@ -1623,22 +1644,23 @@ constexpr int kShortPF = BKD_SHORT_PF;
 
 // The chunk list [0, n) (crc_plan_chunks_kernel): [0, nmain) by long_chunks_loop, then the short
 // tail [nmain, n) by short_chunks_loop (nmain == n: no short tail).
-template <int G, int PF, bool NT>
+template <int G, int PF, bool NT, class Desc>
 __device__ __forceinline__ void plan_chunks_loop(const uint32_t* lds, uint32_t lanereg, int g,
-                                                 const uint8_t* __restrict__ base, const PlanDesc* __restrict__ descs,
+                                                 const uint8_t* __restrict__ base, const Desc* __restrict__ descs,
+                                                 uint32_t r0h,
                                                  uint64_t n, uint64_t nmain, uint64_t gid, uint64_t ngroups,
                                                  uint32_t* __restrict__ out, uint32_t* __restrict__ partials) {
 #if BKD_SHORT_FIRST
     // the short tail first: the long loop's held partials (the larger set) are then stored at the
     // group's very end (per-group work, and so the kernel's balance, does not depend on the order)
     if (nmain < n && gid < n - nmain)
-        short_chunks_loop<G, kShortPF, NT && BKD_SHORT_NT>(lds, lanereg, g, base, descs, nmain + gid, n, ngroups, out,
+        short_chunks_loop<G, kShortPF, NT && BKD_SHORT_NT>(lds, lanereg, g, base, descs, r0h, nmain + gid, n, ngroups, out,
                                                           partials, nmain);
-    if (gid < nmain) long_chunks_loop<G, PF, NT>(lds, lanereg, g, base, descs, nmain, gid, ngroups, out, partials);
+    if (gid < nmain) long_chunks_loop<G, PF, NT>(lds, lanereg, g, base, descs, r0h, nmain, gid, ngroups, out, partials);
 #else
-    if (gid < nmain) long_chunks_loop<G, PF, NT>(lds, lanereg, g, base, descs, nmain, gid, ngroups, out, partials);
+    if (gid < nmain) long_chunks_loop<G, PF, NT>(lds, lanereg, g, base, descs, r0h, nmain, gid, ngroups, out, partials);
     if (nmain < n && gid < n - nmain)
-        short_chunks_loop<G, kShortPF, NT && BKD_SHORT_NT>(lds, lanereg, g, base, descs, nmain + gid, n, ngroups, out,
+        short_chunks_loop<G, kShortPF, NT && BKD_SHORT_NT>(lds, lanereg, g, base, descs, r0h, nmain + gid, n, ngroups, out,
                                                           partials, nmain);
 #endif
 }
@@ -1649,9 +1671,9 @@ __device__ __forceinline__ void plan_chunks_loop(const uint32_t* lds, uint32_t l
 // chunk's first loads are issued during the previous chunk (chunk_fold), X/Y register sets
 // alternating.
 // After its chunks, the grid computes the entries the plan could not hold (`ov`, normally empty).
-template <int G, int PF, bool NT, class OvSrc>
+template <int G, int PF, bool NT, class OvSrc, class Desc = PlanDesc>
 __global__ void __launch_bounds__(kBlock) crc_plan_chunks_kernel(const uint8_t* __restrict__ base,
-                                                                 const PlanDesc* __restrict__ descs,
+                                                                 const Desc* __restrict__ descs, uint32_t r0h,
                                                                  const uint32_t* __restrict__ count,
                                                                  const uint32_t* __restrict__ tables,
                                                                  uint32_t* __restrict__ out,
@@ -1674,7 +1696,7 @@ __global__ void __launch_bounds__(kBlock) crc_plan_chunks_kernel(const uint8_t* 
     const uint64_t gid = (uint64_t)blockIdx.x * (kBlock / G) + (uint64_t)(threadIdx.x / G);
     // count[1]: the list position of the first chunk of at most PF + 1 steps (plan_emit_kernel)
     const uint64_t nmain = n ? std::min<uint64_t>(n, count[1]) : 0u;
-    if (gid < n) plan_chunks_loop<G, PF, NT>(lds, lanereg, g, base, descs, n, nmain, gid, ngroups, out, partials);
+    if (gid < n) plan_chunks_loop<G, PF, NT>(lds, lanereg, g, base, descs, r0h, n, nmain, gid, ngroups, out, partials);
 #if BKD_HOLD_DIRECT > 0
     // near-uniform batches (every entry here, one per group): results held as the uniform kernel's
     if (nov && ov.all) {

@@ -50,6 +50,7 @@ struct PlanGeo {
     uint32_t small;    // entries of <= small bytes belong to the short-entry launch (0: none do)
     uint32_t serial;   // entries shorter than this (16 .. kSerialMax) are computed by plan_combine
     uint32_t jshort;   // chunks of <= jshort steps form the chunk kernel's short tail (PF + 1; 0: none)
+    uint32_t d8;       // 8-byte descriptors (PlanDesc8: unseeded batch, no final chunks)
 };
 
 // Longest entry plan_combine computes itself, one thread per entry (serial_crc).
@@ -112,7 +113,7 @@ __device__ __forceinline__ EntryPlan plan_entry(uint64_t o, uint32_t l, uint64_t
     p.m = m;
     p.jh = (hl + pg.step - 1u) >> pg.step_sh;
     p.full = (m - 1u) + (p.jh == pg.jc ? 1u : 0u);
-    p.ps = (m == 1u && p.pad == 0u) ? 0u : m;
+    p.ps = (m == 1u && p.pad == 0u && !pg.d8) ? 0u : m;  // (PlanDesc8 has no final chunks)
     p.kind = 0;
     return p;
 }
@@ -127,7 +128,8 @@ __device__ __forceinline__ PlanDesc chunk_desc(const EntryPlan& p, uint32_t c, u
     const uint32_t len = (uint32_t)(e - s);
     const uint32_t J = (len + pg.step - 1u) >> pg.step_sh;
     const int64_t w = e - (int64_t)J * (int64_t)pg.step;  // the chunk's step-aligned window start
-    d.s_len = (uint64_t)(w + kWBias) | (pad << kPlanOffBits) | ((uint64_t)len << 48);
+    d.s_len = (uint64_t)(w + kWBias) | (pad << kPlanOffBits) | ((uint64_t)len << 48) |
+              ((pg.d8 && head) ? 1ull << kPlanHeadBit : 0ull);
     d.r0 = head ? ~seed : 0u;
     d.dst = p.ps == 0u ? (entry | kPlanFinal) : slot;  // slot: the chunk's own list position
     return d;
@@ -138,6 +140,12 @@ __device__ __forceinline__ PlanDesc chunk_desc(const EntryPlan& p, uint32_t c, u
 // within the first 16 * G bytes: a plan only overflows with multi-chunk entries, so base holds more
 // than one chunk then).
 __device__ __forceinline__ PlanDesc skip_desc() { return PlanDesc{(uint64_t)kWBias, 0u, 0u}; }
+
+// A descriptor into the list: 16 bytes, or its first word (PlanDesc8) when the plan uses those.
+__device__ __forceinline__ void put_desc(PlanDesc* descs, uint64_t pos, const PlanDesc& d, const PlanGeo& pg) {
+    if (pg.d8) reinterpret_cast<PlanDesc8*>(descs)[pos] = PlanDesc8{d.s_len};
+    else descs[pos] = d;
+}
 
 // Deterministic block-wide exclusive scan (1024 threads = 16 waves).
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t& total) {
@@ -385,7 +393,7 @@ __global__ void __launch_bounds__(kPlanBlock, BKD_PLAN_OCC) plan_emit_kernel(con
         if (rep == 0u) pslot[i] = overflow ? kDirect : (p.ps ? (p.full ? rs : hpos) : kNoSlot);
         if (rep == 0u && p.ps && p.full && has_head) hslot[i] = hpos;
         if (rep == 0u && has_head && (uint64_t)hpos < capacity)
-            descs[hpos] = overflow ? skip_desc() : chunk_desc(p, p.m - 1u, seed, (uint32_t)i, hpos, pg);
+            put_desc(descs, hpos, overflow ? skip_desc() : chunk_desc(p, p.m - 1u, seed, (uint32_t)i, hpos, pg), pg);
         st_ae[threadIdx.x] = p.ae;
         st_s[threadIdx.x] = p.s;
         st_m[threadIdx.x] = p.m;
@@ -417,10 +425,11 @@ __global__ void __launch_bounds__(kPlanBlock, BKD_PLAN_OCC) plan_emit_kernel(con
         const uint64_t pos = (uint64_t)run0 + k;
         const uint32_t fl = st_flags[t];
         if (fl & 0x200u) {
-            if (pos < capacity) descs[pos] = skip_desc();
+            if (pos < capacity) put_desc(descs, pos, skip_desc(), pg);
         } else {
-            descs[pos] = chunk_desc_of(st_ae[t], st_s[t], st_m[t], fl & 0xFFu, (fl & 0x100u) != 0u, c, st_seed[t],
-                                       (uint32_t)((uint64_t)eb * kPlanBlock + t), (uint32_t)pos, pg);
+            put_desc(descs, pos, chunk_desc_of(st_ae[t], st_s[t], st_m[t], fl & 0xFFu, (fl & 0x100u) != 0u, c,
+                                               st_seed[t], (uint32_t)((uint64_t)eb * kPlanBlock + t), (uint32_t)pos, pg),
+                     pg);
         }
     }
     __syncthreads();  // LDS stashes and cursors are rewritten by the next virtual block
