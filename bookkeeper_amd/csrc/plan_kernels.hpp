@@ -13,8 +13,9 @@
 //  * lists the chunks in descending step count (merged heads JC+1, full chunks JC, heads JC-1..1)
 //    so that neighbouring groups, which run in lockstep, have equal work;
 //  * writes one self-contained 16-byte descriptor per chunk (PlanDesc: window, pad, length, seed
-//    register, destination), which the chunk kernel reads two rounds ahead (six chunks ahead in its
-//    short tail) — no dependent index loads at chunk start;
+//    register, destination; 8 bytes, PlanDesc8, for a batch without per-entry seeds), which the chunk
+//    kernel reads two rounds ahead (six chunks ahead in its short tail) — no dependent index loads at
+//    chunk start;
 //  * combines multi-chunk entries as reg = sum_c partial_c * X^c, X = x^(8*CH) (Horner from the
 //    head), then removes the zero padding (multiply by x^(-8*pad)): the GPU analogue of
 //    crc32c_chunk's stream merge by shift tables (crc32c_sse42.cpp:92-134).
